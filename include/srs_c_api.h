@@ -1,0 +1,150 @@
+/*
+ * srs_c_api.h — C ABI of the MI355X-native MSB radix sort (libsrs_amd.so).
+ *
+ * This is the drop-in boundary for the reference's hot path. Every entry point
+ * takes plain pointers and sizes; there are no C++ or torch types in the
+ * signatures, so cgo / ctypes / JNI / N-API can bind it directly.
+ *
+ * Reference interfaces replaced (jonicho/simd-radix-sort, /root/reference):
+ *   srs_sort_soa     <- simd_sort::radix_sort::sort(num, keys, payloads...)
+ *                       radixSort.hpp:1780-1783, and the thresholded form
+ *                       sort<Up,BitSorter,CmpSorter>(cmpSortThreshold, num,
+ *                       keys, payloads...) radixSort.hpp:1761-1768
+ *                       (src/radix_sort.hpp:297-312, :334-337)
+ *   srs_sort_aos     <- sort<Up,BitSorter,CmpSorter>(cmpSortThreshold, num,
+ *                       DataElement<K,Ps...>* elements) radixSort.hpp:1770-1778
+ *                       (src/radix_sort.hpp:314-332)
+ *   *_device         <- same semantics on arrays already resident in HBM,
+ *                       enqueued on a caller-provided hipStream_t.
+ *
+ * Semantics (identical to the reference):
+ *   - In place: on return the caller's arrays hold the sorted data.
+ *   - Key order is the reference's per-bit direction order
+ *     (bitDirUp, radixSort.hpp:1568-1581): unsigned ascending, two's
+ *     complement signed, IEEE floats by value with -0.0 before +0.0 (n >
+ *     cmp_sort_threshold) or -0.0 == +0.0 kept in input order (n <=
+ *     cmp_sort_threshold, the reference's insertion-sort leaf,
+ *     radixSort.hpp:159-178 / :1743). up == 0 reverses the order.
+ *   - num <= 1 is a no-op (radixSort.hpp:1740). num < 0 is a no-op.
+ *   - Payload order inside a run of equal keys: the GPU sort is STABLE
+ *     (input order). The reference is unstable there; see DESIGN.md §5 for
+ *     what parity means for equal keys.
+ *   - NaN keys are outside the contract (the reference's leaf never moves
+ *     them; its output depends on leaf boundaries).
+ *
+ * Error convention: every function returns SRS_OK (0) or a negative
+ * srs_status; srs_last_error() returns a thread-local message. The reference
+ * API is void (no error channel); the C++ drop-in header
+ * (include/simd_sort/radix_sort.hpp) turns a non-zero status into
+ * std::abort() with the message, i.e. it fails loudly. There is NO CPU
+ * fallback inside the library.
+ */
+#ifndef SRS_C_API_H_
+#define SRS_C_API_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Key kinds: the ten key types the reference supports and tests
+ * (src/test.cpp:156-169). Values are part of the ABI. */
+typedef enum srs_key_kind {
+  SRS_KEY_U8 = 0,
+  SRS_KEY_I8 = 1,
+  SRS_KEY_U16 = 2,
+  SRS_KEY_I16 = 3,
+  SRS_KEY_U32 = 4,
+  SRS_KEY_I32 = 5,
+  SRS_KEY_U64 = 6,
+  SRS_KEY_I64 = 7,
+  SRS_KEY_F32 = 8,
+  SRS_KEY_F64 = 9
+} srs_key_kind;
+
+typedef enum srs_status {
+  SRS_OK = 0,
+  SRS_ERR_INVALID_ARG = -1,
+  SRS_ERR_UNSUPPORTED = -2,
+  SRS_ERR_HIP = -3,
+  SRS_ERR_OUT_OF_MEMORY = -4,
+  SRS_ERR_NO_DEVICE = -5,
+  SRS_ERR_INTERNAL = -6
+} srs_status;
+
+/* Maximum number of payload columns per call (the reference's test uses up
+ * to 63 one-byte payloads, src/test.cpp:125-134). */
+#define SRS_MAX_PAYLOADS 64
+
+/* ---- host-pointer drop-in entry points (synchronous) -------------------- */
+
+/* Sort `num` keys (kind `key_kind`) and `num_payloads` payload columns in
+ * place. payload_sizes[i] is the element size in bytes of column i
+ * (1, 2, 4 or 8). cmp_sort_threshold is the reference's cmpSortThreshold
+ * (16 in the two-argument sort()). Host memory; copies through HBM. */
+int srs_sort_soa(int64_t num, int key_kind, int up, int64_t cmp_sort_threshold,
+                 void* keys, int32_t num_payloads, void* const* payloads,
+                 const uint32_t* payload_sizes);
+
+/* Sort `num` combined elements of `elem_size` bytes (a power of two, 1..64,
+ * >= the key size) whose key of kind `key_kind` sits at byte offset 0
+ * (simd_sort::DataElement<K, Ps...>). The payload bytes are opaque and move
+ * with their key. */
+int srs_sort_aos(int64_t num, int key_kind, int up, int64_t cmp_sort_threshold,
+                 void* elements, uint32_t elem_size);
+
+/* ---- device-pointer entry points (asynchronous on `stream`) ------------- */
+
+/* Same as srs_sort_soa on device pointers. `stream` is a hipStream_t (NULL =
+ * the default stream). If keys_out/payloads_out are NULL the sort is in place;
+ * otherwise the inputs are left untouched and the result is written to the
+ * *_out arrays (which must not alias the inputs). The call enqueues work and
+ * may block briefly on small control read-backs; results are ready when the
+ * stream completes. */
+int srs_sort_soa_device(int64_t num, int key_kind, int up,
+                        int64_t cmp_sort_threshold, void* keys,
+                        int32_t num_payloads, void* const* payloads,
+                        const uint32_t* payload_sizes, void* keys_out,
+                        void* const* payloads_out, void* stream);
+
+int srs_sort_aos_device(int64_t num, int key_kind, int up,
+                        int64_t cmp_sort_threshold, void* elements,
+                        uint32_t elem_size, void* elements_out, void* stream);
+
+/* ---- synthetic data (bench / tests) ------------------------------------- */
+
+/* keys[i] = splitmix64(seed + first_index + i) truncated/reinterpreted to the
+ * key kind (floats: uniform in [-1,1) on a 2^-23 / 2^-52 grid); payload column
+ * c gets bytes of splitmix64(bits(key[i]) + c) (a function of the key). */
+int srs_fill_synthetic_device(int64_t num, int key_kind, uint64_t seed,
+                              uint64_t first_index, void* keys,
+                              int32_t num_payloads, void* const* payloads,
+                              const uint32_t* payload_sizes, void* stream);
+
+/* ---- diagnostics ---------------------------------------------------------- */
+
+/* Thread-local description of the last error (never NULL). */
+const char* srs_last_error(void);
+
+/* Library version string ("srs_amd <semver> gfx950"). */
+const char* srs_version(void);
+
+/* Per-kernel timing with HIP events recorded on the launch stream around
+ * every kernel launch (off by default). srs_kernel_stats fills, for kernel
+ * name `name` ("count", "scatter", "local", "scan", ...), the number of
+ * launches and the summed device milliseconds since the last reset; the
+ * stream must have completed. Returns SRS_ERR_INVALID_ARG for unknown names. */
+int srs_set_kernel_timing(int enable);
+int srs_reset_kernel_stats(void);
+int srs_kernel_stats(const char* name, int64_t* launches, double* total_ms,
+                     double* elements);
+
+/* Release cached device workspaces (for leak checks / shutdown). */
+int srs_release_workspace(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SRS_C_API_H_ */

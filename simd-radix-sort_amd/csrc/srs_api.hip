@@ -1,0 +1,652 @@
+// srs_api.hip — C ABI (include/srs_c_api.h) and the host-side level driver.
+//
+// Drop-in for simd_sort::radix_sort::sort (radixSort.hpp:1761-1783): the
+// caller's arrays are sorted in place; the host-pointer entry points stage
+// through HBM. The driver walks the MSB levels breadth-first:
+//
+//   big segments (> kLocalCap keys):  plan -> scan -> tile map -> count ->
+//       scan -> children -> scatter     (one launch each per level)
+//   small segments:                    local LDS sort (one launch at the end)
+//   finished, not in OUT:              D2D copy
+//
+// Two small control read-backs per level (tile/histogram totals, list
+// counters) size the next launches. Everything else stays on the device.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <map>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/srs_c_api.h"
+#include "srs_common.h"
+#include "srs_kernels.h"
+
+namespace srs {
+namespace {
+
+thread_local std::string g_err = "no error";
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                            \
+  do {                                                                           \
+    hipError_t e_ = (expr);                                                      \
+    if (e_ != hipSuccess)                                                        \
+      return fail(e_ == hipErrorOutOfMemory ? SRS_ERR_OUT_OF_MEMORY : SRS_ERR_HIP, \
+                  std::string(#expr " -> ") + hipGetErrorString(e_));            \
+  } while (0)
+
+#define SRS_TRY(expr)          \
+  do {                         \
+    int r_ = (expr);           \
+    if (r_ != SRS_OK) return r_; \
+  } while (0)
+
+int key_size_of(int kind) {
+  switch (kind) {
+    case SRS_KEY_U8: case SRS_KEY_I8: return 1;
+    case SRS_KEY_U16: case SRS_KEY_I16: return 2;
+    case SRS_KEY_U32: case SRS_KEY_I32: case SRS_KEY_F32: return 4;
+    case SRS_KEY_U64: case SRS_KEY_I64: case SRS_KEY_F64: return 8;
+    default: return 0;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// kernel timing (optional; HIP events around every launch on its stream)
+// ---------------------------------------------------------------------------
+struct TimingRec {
+  std::string name;
+  hipEvent_t a, b;
+  double elems;
+};
+struct KStat {
+  int64_t launches = 0;
+  double ms = 0;
+  double elems = 0;
+};
+std::mutex g_tmu;
+bool g_timing = false;
+std::vector<TimingRec> g_pending;
+std::vector<hipEvent_t> g_event_pool;
+std::map<std::string, KStat> g_stats;
+
+hipEvent_t get_event() {
+  if (!g_event_pool.empty()) {
+    hipEvent_t e = g_event_pool.back();
+    g_event_pool.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  if (hipEventCreate(&e) != hipSuccess) return nullptr;
+  return e;
+}
+
+struct TimedScope {
+  bool on = false;
+  TimingRec rec;
+  hipStream_t st;
+  TimedScope(const char* name, double elems, hipStream_t s) : st(s) {
+    std::lock_guard<std::mutex> lk(g_tmu);
+    if (!g_timing) return;
+    rec.name = name;
+    rec.elems = elems;
+    rec.a = get_event();
+    rec.b = get_event();
+    if (!rec.a || !rec.b) return;
+    on = hipEventRecord(rec.a, st) == hipSuccess;
+  }
+  ~TimedScope() {
+    if (!on) return;
+    std::lock_guard<std::mutex> lk(g_tmu);
+    if (hipEventRecord(rec.b, st) == hipSuccess) g_pending.push_back(rec);
+  }
+};
+
+void note_elems(const char* name, double elems) {
+  std::lock_guard<std::mutex> lk(g_tmu);
+  if (g_timing) g_stats[name].elems += elems;
+}
+
+void drain_timing_locked() {
+  for (auto& r : g_pending) {
+    float ms = 0;
+    if (hipEventSynchronize(r.b) == hipSuccess &&
+        hipEventElapsedTime(&ms, r.a, r.b) == hipSuccess) {
+      KStat& k = g_stats[r.name];
+      k.launches++;
+      k.ms += ms;
+      k.elems += r.elems;
+    }
+    g_event_pool.push_back(r.a);
+    g_event_pool.push_back(r.b);
+  }
+  g_pending.clear();
+}
+
+// ---------------------------------------------------------------------------
+// per-device workspace (grown on demand, reused across calls)
+// ---------------------------------------------------------------------------
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+};
+
+int ensure(DevBuf& b, size_t bytes) {
+  if (b.bytes >= bytes && b.p) return SRS_OK;
+  if (b.p) {
+    HIP_TRY(hipFree(b.p));
+    b.p = nullptr;
+    b.bytes = 0;
+  }
+  size_t want = std::max<size_t>(bytes, 256);
+  HIP_TRY(hipMalloc(&b.p, want));
+  b.bytes = want;
+  return SRS_OK;
+}
+
+// Growing a list that already holds live entries (copy then swap).
+int ensure_keep(DevBuf& b, size_t bytes, size_t live_bytes, hipStream_t st) {
+  if (b.bytes >= bytes && b.p) return SRS_OK;
+  DevBuf nb;
+  size_t want = std::max<size_t>(bytes, b.bytes * 2);
+  HIP_TRY(hipMalloc(&nb.p, want));
+  nb.bytes = want;
+  if (b.p && live_bytes) HIP_TRY(hipMemcpyAsync(nb.p, b.p, live_bytes, hipMemcpyDeviceToDevice, st));
+  if (b.p) {
+    HIP_TRY(hipStreamSynchronize(st));
+    HIP_TRY(hipFree(b.p));
+  }
+  b = nb;
+  return SRS_OK;
+}
+
+struct Workspace {
+  DevBuf tmp;         // TMP data buffer (same footprint as the input)
+  DevBuf stage;       // device copy of host arrays (host-pointer API)
+  DevBuf desc;        // SortDesc
+  DevBuf big[2], local, copy;
+  DevBuf plan, tcount, hcount, tbase, hbase, var;
+  DevBuf tile_seg, hist, scan_tmp, totals, ctr;
+  ListCounters* h_ctr = nullptr;
+  uint64_t* h_totals = nullptr;
+};
+
+std::mutex g_wmu;
+std::map<int, Workspace*> g_ws;
+
+int get_ws(Workspace** out) {
+  int dev = 0;
+  HIP_TRY(hipGetDevice(&dev));
+  auto it = g_ws.find(dev);
+  if (it != g_ws.end()) {
+    *out = it->second;
+    return SRS_OK;
+  }
+  Workspace* w = new Workspace();
+  HIP_TRY(hipHostMalloc((void**)&w->h_ctr, sizeof(ListCounters), hipHostMallocDefault));
+  HIP_TRY(hipHostMalloc((void**)&w->h_totals, 4 * sizeof(uint64_t), hipHostMallocDefault));
+  g_ws[dev] = w;
+  *out = w;
+  return SRS_OK;
+}
+
+size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+// ---------------------------------------------------------------------------
+// the sort driver (device pointers)
+// ---------------------------------------------------------------------------
+struct Request {
+  int64_t num;
+  int kind;
+  int up;
+  int64_t thresh;
+  bool aos;
+  uint32_t elem_size;                // AoS record size
+  void* in_cols[SRS_MAX_PAYLOADS + 1];
+  void* out_cols[SRS_MAX_PAYLOADS + 1];
+  uint32_t widths[SRS_MAX_PAYLOADS + 1];
+  int ncols;                         // SoA: 1 + payloads; AoS: 1
+};
+
+void key_masks(int kind, int up, SortDesc& d) {
+  const int kb = 8 * key_size_of(kind);
+  const uint64_t all = kb == 64 ? ~0ull : ((1ull << kb) - 1);
+  const uint64_t sb = 1ull << (kb - 1);
+  uint64_t mpos = 0, mneg = 0;
+  switch (kind) {
+    case SRS_KEY_U8: case SRS_KEY_U16: case SRS_KEY_U32: case SRS_KEY_U64:
+      mpos = mneg = 0;
+      break;
+    case SRS_KEY_F32: case SRS_KEY_F64:
+      mpos = sb;   // non-negative: flip sign bit
+      mneg = all;  // negative: flip everything
+      break;
+    default:       // signed
+      mpos = mneg = sb;
+      break;
+  }
+  if (!up) {
+    mpos ^= all;
+    mneg ^= all;
+  }
+  d.mpos = mpos;
+  d.mneg = mneg;
+  d.signbit = sb;
+  d.negzero = sb;  // bit pattern of -0.0
+  d.key_bits = kb;
+}
+
+int run_sort(Workspace* W, const Request& R, hipStream_t st) {
+  const int ks = key_size_of(R.kind);
+  const int64_t n = R.num;
+  bool inplace = true;
+  for (int c = 0; c < R.ncols; c++) inplace &= (R.in_cols[c] == R.out_cols[c]);
+
+  // ---- descriptor: key view + columns (AoS records as <= 8-byte slices) --
+  SortDesc d;
+  memset(&d, 0, sizeof d);
+  key_masks(R.kind, R.up, d);
+  const bool is_float = R.kind == SRS_KEY_F32 || R.kind == SRS_KEY_F64;
+  d.canon_zero = (is_float && n <= R.thresh) ? 1 : 0;
+
+  size_t tmp_bytes = 0;
+  std::vector<size_t> tmp_off;
+  if (R.aos) {
+    tmp_off.push_back(0);
+    tmp_bytes = align_up((size_t)n * R.elem_size, 256);
+  } else {
+    for (int c = 0; c < R.ncols; c++) {
+      tmp_off.push_back(tmp_bytes);
+      tmp_bytes += align_up((size_t)n * R.widths[c], 256);
+    }
+  }
+  SRS_TRY(ensure(W->tmp, tmp_bytes));
+  char* tmp = (char*)W->tmp.p;
+
+  if (R.aos) {
+    const uint32_t E = R.elem_size;
+    char* in = (char*)R.in_cols[0];
+    char* out = (char*)R.out_cols[0];
+    d.key = Col{{in, out, tmp}, (uint32_t)ks, E};
+    const uint32_t slice = E < 8 ? E : 8;
+    int nc = 0;
+    for (uint32_t off = 0; off < E; off += slice) {
+      d.cols[nc++] = Col{{in + off, out + off, tmp + off}, slice, E};
+    }
+    d.ncols = nc;
+    d.col0_is_key = 0;
+  } else {
+    for (int c = 0; c < R.ncols; c++) {
+      d.cols[c] = Col{{(char*)R.in_cols[c], (char*)R.out_cols[c], tmp + tmp_off[c]},
+                      R.widths[c], R.widths[c]};
+    }
+    d.key = d.cols[0];
+    d.ncols = R.ncols;
+    d.col0_is_key = 1;
+  }
+  if (inplace)  // IN aliases OUT: a segment that never moved is already home
+    for (int c = 0; c < d.ncols; c++) d.cols[c].base[BUF_IN] = d.cols[c].base[BUF_OUT];
+
+  SRS_TRY(ensure(W->desc, sizeof(SortDesc)));
+  SortDesc* d_desc = (SortDesc*)W->desc.p;
+  launch_set_desc(d, d_desc, st);
+
+  // ---- initial segment -----------------------------------------------------
+  Seg seg0{0, n, d.key_bits, inplace ? BUF_OUT : BUF_IN};
+  const bool to_local = n <= kLocalCap;
+  size_t big_cap = 1024, local_cap = 1024, copy_cap = 1024;
+  SRS_TRY(ensure(W->big[0], big_cap * sizeof(Seg)));
+  SRS_TRY(ensure(W->big[1], big_cap * sizeof(Seg)));
+  SRS_TRY(ensure(W->local, local_cap * sizeof(Seg)));
+  SRS_TRY(ensure(W->copy, copy_cap * sizeof(Seg)));
+  SRS_TRY(ensure(W->ctr, sizeof(ListCounters)));
+  SRS_TRY(ensure(W->totals, 4 * sizeof(uint64_t)));
+  ListCounters* d_ctr = (ListCounters*)W->ctr.p;
+  uint64_t* d_totals = (uint64_t*)W->totals.p;
+  launch_init_lists(seg0, to_local ? 1 : 0, (Seg*)W->big[0].p, (Seg*)W->local.p, d_ctr, st);
+
+  int64_t nbig = to_local ? 0 : 1;
+  int64_t n_local = to_local ? 1 : 0, n_copy = 0;
+  int cur = 0;
+  int level = 0;
+  while (nbig > 0) {
+    if (++level > 80) return fail(SRS_ERR_INTERNAL, "level limit exceeded");
+    // ---- plan + tile / histogram bases
+    SRS_TRY(ensure(W->plan, nbig * sizeof(SegPlan)));
+    SRS_TRY(ensure(W->tcount, nbig * 8));
+    SRS_TRY(ensure(W->hcount, nbig * 8));
+    SRS_TRY(ensure(W->tbase, nbig * 8));
+    SRS_TRY(ensure(W->hbase, nbig * 8));
+    SRS_TRY(ensure(W->var, nbig * 8));
+    SRS_TRY(ensure(W->scan_tmp, scan_temp_elems(nbig) * 8));
+    SegPlan* plan = (SegPlan*)W->plan.p;
+    unsigned long long* var = (unsigned long long*)W->var.p;
+    {
+      TimedScope ts("plan", (double)nbig, st);
+      HIP_TRY(hipMemsetAsync(d_totals + 3, 0, sizeof(uint64_t), st));
+      launch_plan((Seg*)W->big[cur].p, nbig, plan, (int64_t*)W->tcount.p,
+                  (int64_t*)W->hcount.p, var, d_totals + 3, st);
+      launch_excl_scan((uint64_t*)W->tcount.p, (uint64_t*)W->tbase.p, nbig,
+                       (uint64_t*)W->scan_tmp.p, d_totals + 0, st);
+      launch_excl_scan((uint64_t*)W->hcount.p, (uint64_t*)W->hbase.p, nbig,
+                       (uint64_t*)W->scan_tmp.p, d_totals + 1, st);
+      launch_plan_bases(plan, nbig, (int64_t*)W->tbase.p, (int64_t*)W->hbase.p, st);
+    }
+    HIP_TRY(hipMemcpyAsync(W->h_totals, d_totals, 4 * sizeof(uint64_t),
+                           hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    const int64_t ntiles = (int64_t)W->h_totals[0];
+    const int64_t nhist = (int64_t)W->h_totals[1];
+    const double level_elems = (double)W->h_totals[3];
+    note_elems("count", level_elems);
+    note_elems("scatter", level_elems);
+
+    SRS_TRY(ensure(W->tile_seg, ntiles * 4));
+    SRS_TRY(ensure(W->hist, nhist * 8));
+    SRS_TRY(ensure(W->scan_tmp, scan_temp_elems(std::max(nhist, nbig)) * 8));
+    int32_t* tile_seg = (int32_t*)W->tile_seg.p;
+    uint64_t* hist = (uint64_t*)W->hist.p;
+    launch_tile_map(plan, nbig, ntiles, tile_seg, st);
+    {
+      TimedScope ts("count", (double)0, st);
+      launch_count(ks, d_desc, plan, tile_seg, ntiles, hist, var, st);
+    }
+    {
+      TimedScope ts("scan", (double)nhist, st);
+      launch_excl_scan(hist, hist, nhist, (uint64_t*)W->scan_tmp.p, d_totals + 2, st);
+    }
+    // ---- children (list capacity for the worst case: every bin non-empty)
+    const size_t worst = (size_t)nbig * kMaxBins;
+    const int nxt = cur ^ 1;
+    SRS_TRY(ensure(W->big[nxt], worst * sizeof(Seg)));
+    SRS_TRY(ensure_keep(W->local, (n_local + worst) * sizeof(Seg), n_local * sizeof(Seg), st));
+    SRS_TRY(ensure_keep(W->copy, (n_copy + worst) * sizeof(Seg), n_copy * sizeof(Seg), st));
+    HIP_TRY(hipMemsetAsync(&d_ctr->n_big, 0, sizeof(unsigned long long), st));
+    {
+      TimedScope ts("children", (double)nbig, st);
+      launch_children(plan, nbig, hist, var, (Seg*)W->big[nxt].p, (Seg*)W->local.p,
+                      (Seg*)W->copy.p, d_ctr, st);
+    }
+    {
+      TimedScope ts("scatter", (double)0, st);
+      launch_scatter(ks, d_desc, plan, tile_seg, hist, ntiles, st);
+    }
+    HIP_TRY(hipMemcpyAsync(W->h_ctr, d_ctr, sizeof(ListCounters), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    nbig = (int64_t)W->h_ctr->n_big;
+    n_local = (int64_t)W->h_ctr->n_local;
+    n_copy = (int64_t)W->h_ctr->n_copy;
+    cur = nxt;
+  }
+
+  if (n_local > 0) {
+    note_elems("local", (double)W->h_ctr->local_elems);
+    TimedScope ts("local", (double)0, st);
+    launch_local(ks, d_desc, (Seg*)W->local.p, n_local, st);
+  }
+  if (n_copy > 0) {
+    std::vector<Seg> cp((size_t)n_copy);
+    HIP_TRY(hipMemcpyAsync(cp.data(), W->copy.p, n_copy * sizeof(Seg),
+                           hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    TimedScope ts("copy", (double)0, st);
+    for (const Seg& g : cp) {
+      if (R.aos) {
+        const size_t E = R.elem_size;
+        HIP_TRY(hipMemcpyAsync(d.cols[0].base[BUF_OUT] + g.start * E,
+                               d.cols[0].base[g.buf] + g.start * E, g.len * E,
+                               hipMemcpyDeviceToDevice, st));
+      } else {
+        for (int c = 0; c < d.ncols; c++) {
+          const size_t w = d.cols[c].width;
+          HIP_TRY(hipMemcpyAsync(d.cols[c].base[BUF_OUT] + g.start * w,
+                                 d.cols[c].base[g.buf] + g.start * w, g.len * w,
+                                 hipMemcpyDeviceToDevice, st));
+        }
+      }
+    }
+  }
+  HIP_TRY(hipGetLastError());
+  return SRS_OK;
+}
+
+int validate_common(int64_t num, int kind) {
+  if (key_size_of(kind) == 0) return fail(SRS_ERR_INVALID_ARG, "invalid key_kind");
+  (void)num;
+  return SRS_OK;
+}
+
+int copy_through(const Request& R, hipStream_t st) {
+  // num <= 1 with distinct output arrays: the result is the input
+  const int64_t n = R.num < 0 ? 0 : R.num;
+  for (int c = 0; c < R.ncols; c++) {
+    if (R.in_cols[c] == R.out_cols[c] || n == 0) continue;
+    const size_t w = R.aos ? R.elem_size : R.widths[c];
+    HIP_TRY(hipMemcpyAsync(R.out_cols[c], R.in_cols[c], n * w, hipMemcpyDeviceToDevice, st));
+  }
+  return SRS_OK;
+}
+
+int sort_device(Request& R, hipStream_t st) {
+  if (R.num <= 1) return copy_through(R, st);
+  std::lock_guard<std::mutex> lk(g_wmu);
+  Workspace* W = nullptr;
+  SRS_TRY(get_ws(&W));
+  return run_sort(W, R, st);
+}
+
+int sort_host(Request& R) {
+  if (R.num <= 1) return SRS_OK;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+    return fail(SRS_ERR_NO_DEVICE, "no HIP device available");
+  std::lock_guard<std::mutex> lk(g_wmu);
+  Workspace* W = nullptr;
+  SRS_TRY(get_ws(&W));
+  // stage every column in HBM (one allocation), sort in place there, copy back
+  std::vector<size_t> off;
+  size_t total = 0;
+  for (int c = 0; c < R.ncols; c++) {
+    off.push_back(total);
+    const size_t w = R.aos ? R.elem_size : R.widths[c];
+    total += align_up((size_t)R.num * w, 256);
+  }
+  SRS_TRY(ensure(W->stage, total));
+  hipStream_t st = nullptr;
+  Request D = R;
+  for (int c = 0; c < R.ncols; c++) {
+    const size_t w = R.aos ? R.elem_size : R.widths[c];
+    char* dp = (char*)W->stage.p + off[c];
+    HIP_TRY(hipMemcpy(dp, R.in_cols[c], (size_t)R.num * w, hipMemcpyHostToDevice));
+    D.in_cols[c] = D.out_cols[c] = dp;
+  }
+  SRS_TRY(run_sort(W, D, st));
+  for (int c = 0; c < R.ncols; c++) {
+    const size_t w = R.aos ? R.elem_size : R.widths[c];
+    HIP_TRY(hipMemcpy(R.out_cols[c], D.out_cols[c], (size_t)R.num * w,
+                      hipMemcpyDeviceToHost));
+  }
+  HIP_TRY(hipDeviceSynchronize());
+  return SRS_OK;
+}
+
+int build_soa(Request& R, int64_t num, int kind, int up, int64_t thresh, void* keys,
+              int32_t np, void* const* pays, const uint32_t* sizes, void* keys_out,
+              void* const* pays_out) {
+  SRS_TRY(validate_common(num, kind));
+  if (np < 0 || np > SRS_MAX_PAYLOADS) return fail(SRS_ERR_INVALID_ARG, "num_payloads out of range");
+  if (num > 1 && !keys) return fail(SRS_ERR_INVALID_ARG, "keys is NULL");
+  if (np > 0 && (!pays || !sizes)) return fail(SRS_ERR_INVALID_ARG, "payload arrays missing");
+  if ((keys_out && np > 0 && !pays_out) || (!keys_out && pays_out))
+    return fail(SRS_ERR_INVALID_ARG, "keys_out and payloads_out must both be set or both NULL");
+  R.num = num;
+  R.kind = kind;
+  R.up = up ? 1 : 0;
+  R.thresh = thresh;
+  R.aos = false;
+  R.elem_size = 0;
+  R.ncols = 1 + np;
+  R.in_cols[0] = keys;
+  R.out_cols[0] = keys_out ? keys_out : keys;
+  R.widths[0] = (uint32_t)key_size_of(kind);
+  for (int i = 0; i < np; i++) {
+    const uint32_t w = sizes[i];
+    if (w != 1 && w != 2 && w != 4 && w != 8)
+      return fail(SRS_ERR_UNSUPPORTED, "payload sizes must be 1, 2, 4 or 8 bytes");
+    if (num > 1 && !pays[i]) return fail(SRS_ERR_INVALID_ARG, "payload pointer is NULL");
+    R.in_cols[1 + i] = pays[i];
+    R.out_cols[1 + i] = keys_out ? pays_out[i] : pays[i];
+    R.widths[1 + i] = w;
+  }
+  return SRS_OK;
+}
+
+int build_aos(Request& R, int64_t num, int kind, int up, int64_t thresh, void* elems,
+              uint32_t esz, void* elems_out) {
+  SRS_TRY(validate_common(num, kind));
+  const int ks = key_size_of(kind);
+  // static_assert(is_power_of_two<sizeof(DataElement<K, Ps...>)>),
+  // radixSort.hpp:1774
+  if (esz < (uint32_t)ks || esz > 64 || (esz & (esz - 1)) != 0)
+    return fail(SRS_ERR_UNSUPPORTED,
+                "elem_size must be a power of two in [sizeof(key), 64]");
+  if (num > 1 && !elems) return fail(SRS_ERR_INVALID_ARG, "elements is NULL");
+  R.num = num;
+  R.kind = kind;
+  R.up = up ? 1 : 0;
+  R.thresh = thresh;
+  R.aos = true;
+  R.elem_size = esz;
+  R.ncols = 1;
+  R.in_cols[0] = elems;
+  R.out_cols[0] = elems_out ? elems_out : elems;
+  R.widths[0] = esz;
+  return SRS_OK;
+}
+
+}  // namespace
+}  // namespace srs
+
+using namespace srs;
+
+extern "C" {
+
+int srs_sort_soa(int64_t num, int key_kind, int up, int64_t cmp_sort_threshold, void* keys,
+                 int32_t num_payloads, void* const* payloads, const uint32_t* payload_sizes) {
+  Request R;
+  SRS_TRY(build_soa(R, num, key_kind, up, cmp_sort_threshold, keys, num_payloads, payloads,
+                    payload_sizes, nullptr, nullptr));
+  return sort_host(R);
+}
+
+int srs_sort_aos(int64_t num, int key_kind, int up, int64_t cmp_sort_threshold,
+                 void* elements, uint32_t elem_size) {
+  Request R;
+  SRS_TRY(build_aos(R, num, key_kind, up, cmp_sort_threshold, elements, elem_size, nullptr));
+  return sort_host(R);
+}
+
+int srs_sort_soa_device(int64_t num, int key_kind, int up, int64_t cmp_sort_threshold,
+                        void* keys, int32_t num_payloads, void* const* payloads,
+                        const uint32_t* payload_sizes, void* keys_out,
+                        void* const* payloads_out, void* stream) {
+  Request R;
+  SRS_TRY(build_soa(R, num, key_kind, up, cmp_sort_threshold, keys, num_payloads, payloads,
+                    payload_sizes, keys_out, payloads_out));
+  return sort_device(R, (hipStream_t)stream);
+}
+
+int srs_sort_aos_device(int64_t num, int key_kind, int up, int64_t cmp_sort_threshold,
+                        void* elements, uint32_t elem_size, void* elements_out,
+                        void* stream) {
+  Request R;
+  SRS_TRY(build_aos(R, num, key_kind, up, cmp_sort_threshold, elements, elem_size,
+                    elements_out));
+  return sort_device(R, (hipStream_t)stream);
+}
+
+int srs_fill_synthetic_device(int64_t num, int key_kind, uint64_t seed, uint64_t first_index,
+                              void* keys, int32_t num_payloads, void* const* payloads,
+                              const uint32_t* payload_sizes, void* stream) {
+  if (key_size_of(key_kind) == 0) return fail(SRS_ERR_INVALID_ARG, "invalid key_kind");
+  if (num_payloads < 0 || num_payloads > SRS_MAX_PAYLOADS)
+    return fail(SRS_ERR_INVALID_ARG, "num_payloads out of range");
+  if (num <= 0) return SRS_OK;
+  hipStream_t st = (hipStream_t)stream;
+  Col cols[SRS_MAX_PAYLOADS];
+  for (int i = 0; i < num_payloads; i++) {
+    const uint32_t w = payload_sizes[i];
+    if (w != 1 && w != 2 && w != 4 && w != 8)
+      return fail(SRS_ERR_UNSUPPORTED, "payload sizes must be 1, 2, 4 or 8 bytes");
+    cols[i] = Col{{(char*)payloads[i], nullptr, nullptr}, w, w};
+  }
+  void* d_cols = nullptr;
+  if (num_payloads > 0) {
+    HIP_TRY(hipMalloc(&d_cols, sizeof(Col) * num_payloads));
+    HIP_TRY(hipMemcpy(d_cols, cols, sizeof(Col) * num_payloads, hipMemcpyHostToDevice));
+  }
+  launch_fill(num, key_kind, seed, first_index, keys, num_payloads, (const Col*)d_cols, st);
+  HIP_TRY(hipGetLastError());
+  if (d_cols) {
+    HIP_TRY(hipStreamSynchronize(st));
+    HIP_TRY(hipFree(d_cols));
+  }
+  return SRS_OK;
+}
+
+const char* srs_last_error(void) { return g_err.c_str(); }
+
+const char* srs_version(void) { return "srs_amd 0.1.0 gfx950"; }
+
+int srs_set_kernel_timing(int enable) {
+  std::lock_guard<std::mutex> lk(g_tmu);
+  g_timing = enable != 0;
+  return SRS_OK;
+}
+
+int srs_reset_kernel_stats(void) {
+  std::lock_guard<std::mutex> lk(g_tmu);
+  drain_timing_locked();
+  g_stats.clear();
+  return SRS_OK;
+}
+
+int srs_kernel_stats(const char* name, int64_t* launches, double* total_ms, double* elements) {
+  std::lock_guard<std::mutex> lk(g_tmu);
+  drain_timing_locked();
+  if (!name) return fail(SRS_ERR_INVALID_ARG, "name is NULL");
+  auto it = g_stats.find(name);
+  const KStat k = it == g_stats.end() ? KStat{} : it->second;
+  if (launches) *launches = k.launches;
+  if (total_ms) *total_ms = k.ms;
+  if (elements) *elements = k.elems;
+  return SRS_OK;
+}
+
+int srs_release_workspace(void) {
+  std::lock_guard<std::mutex> lk(g_wmu);
+  for (auto& kv : g_ws) {
+    Workspace* w = kv.second;
+    DevBuf* bufs[] = {&w->tmp, &w->stage, &w->desc, &w->big[0], &w->big[1], &w->local,
+                      &w->copy, &w->plan, &w->tcount, &w->hcount, &w->tbase, &w->hbase,
+                      &w->var, &w->tile_seg, &w->hist, &w->scan_tmp, &w->totals, &w->ctr};
+    for (DevBuf* b : bufs)
+      if (b->p) (void)hipFree(b->p);
+    (void)hipHostFree(w->h_ctr);
+    (void)hipHostFree(w->h_totals);
+    delete w;
+  }
+  g_ws.clear();
+  return SRS_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,86 @@
+// srs_common.h — data layout shared by the HIP kernels and the host driver.
+//
+// The sort is an MSB radix sort organised breadth-first over "segments"
+// (contiguous index ranges whose keys agree on all bits above `rbits`):
+//
+//   * global digit pass (count -> scan -> scatter) for segments larger than
+//     the LDS capacity; one launch handles every large segment of a level;
+//   * local LDS sort (one workgroup per segment) for segments that fit.
+//
+// This replaces the reference's depth-first 1-bit recursion
+// (radixRecursion, radixSort.hpp:1734-1759) and its AVX-512 compress-store
+// partition (BitSorterSIMD::sortBit, radixSort.hpp:1587-1686).
+#pragma once
+
+#include <stdint.h>
+
+namespace srs {
+
+// Buffer slots a segment can live in. IN may alias OUT (in-place call).
+enum BufId : int32_t { BUF_IN = 0, BUF_OUT = 1, BUF_TMP = 2 };
+
+// A column of fixed-width elements (the key column, a payload column, or an
+// 8-byte slice of an AoS record). Element i of buffer b lives at
+// base[b] + i * stride, `width` bytes (1, 2, 4 or 8).
+struct Col {
+  char* base[3];
+  uint32_t width;
+  uint32_t stride;
+};
+
+#define SRS_MAX_COLS 72
+
+// Everything a kernel needs to read keys and move records.
+struct SortDesc {
+  Col key;                 // key view (width = key size)
+  Col cols[SRS_MAX_COLS];  // columns moved with every key
+  int32_t ncols;
+  int32_t col0_is_key;     // SoA: cols[0] is the key column (moved from registers)
+  int32_t key_bits;        // 8 * key size
+  int32_t canon_zero;      // float keys, n <= cmpSortThreshold: -0.0 == +0.0
+  // transformed key u = bits ^ (bits & signbit ? mneg : mpos)
+  uint64_t mpos, mneg, signbit, negzero;
+};
+
+struct Seg {
+  int64_t start;
+  int64_t len;
+  int32_t rbits;  // keys agree on transformed bits >= rbits
+  int32_t buf;    // BufId where the segment's data currently lives
+};
+
+// Per large segment, for one global digit pass.
+struct SegPlan {
+  int64_t start;
+  int64_t len;
+  int64_t tile_base;  // first tile of this segment in the level's tile space
+  int64_t hist_base;  // first histogram entry (bin-major: bin * ntiles + tile)
+  int32_t ntiles;
+  int32_t shift;      // digit = (u >> shift) & ((1 << bits) - 1)
+  int32_t bits;
+  int32_t buf;        // source buffer
+  int32_t dst;        // destination buffer of the scatter
+  int32_t skip;       // set by the children kernel: one bucket holds everything
+};
+
+// Work-list counters (device), read back by the host once per level.
+struct ListCounters {
+  unsigned long long n_big;    // segments for the next global level
+  unsigned long long n_local;  // segments for the LDS sort
+  unsigned long long n_copy;   // finished segments that must be copied to OUT
+  unsigned long long local_elems;  // keys in the local list (timing stats)
+};
+
+// Tuning constants (see DESIGN.md §4 for how they were chosen).
+constexpr int kScatterThreads = 512;
+constexpr int kScatterItems = 16;
+constexpr int kTile = kScatterThreads * kScatterItems;   // 8192 keys per tile
+constexpr int kMaxDigitBits = 10;
+constexpr int kMaxBins = 1 << kMaxDigitBits;
+
+constexpr int kLocalThreads = 512;
+constexpr int kLocalItems = 16;
+constexpr int kLocalCap = kLocalThreads * kLocalItems;    // 8192 keys per segment
+constexpr int kLocalTarget = 6144;                        // digit sizing target
+
+}  // namespace srs

@@ -1,0 +1,234 @@
+"""srs_amd — Python mirror of simd_sort::radix_sort over the C ABI of
+libsrs_amd.so (include/srs_c_api.h).
+
+Reference interface mirrored (jonicho/simd-radix-sort, radixSort.hpp):
+  sort(keys, *payloads, up=True)                     radix_sort::sort<Up>(num, keys, payloads...)   :1780
+  sort_thresh(thresh, keys, *payloads, up=True)      sort<Up,BitSorter,CmpSorter>(thresh, num, ...)  :1761
+  sort_combined(elements, key_kind, up=True)         sort(thresh, num, DataElement<K,Ps...>*)         :1770
+
+Host numpy arrays are sorted in place (the reference's contract). The
+*_device functions take torch tensors already resident in HBM and enqueue on
+torch's current stream.
+
+There is no CPU fallback: if the HIP library is missing or the call fails,
+an exception is raised.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+try:  # load torch first so one HIP runtime (torch's) serves both libraries
+    import torch  # noqa: F401
+    _HAVE_TORCH = True
+except Exception:  # pragma: no cover - torch is present in this image
+    _HAVE_TORCH = False
+
+_PKG_ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+LIB_PATH = os.path.join(_PKG_ROOT, "lib", "libsrs_amd.so")
+
+# srs_key_kind (include/srs_c_api.h)
+KEY_U8, KEY_I8, KEY_U16, KEY_I16, KEY_U32, KEY_I32, KEY_U64, KEY_I64, KEY_F32, KEY_F64 = range(10)
+_NP_KIND = {np.dtype(np.uint8): KEY_U8, np.dtype(np.int8): KEY_I8,
+            np.dtype(np.uint16): KEY_U16, np.dtype(np.int16): KEY_I16,
+            np.dtype(np.uint32): KEY_U32, np.dtype(np.int32): KEY_I32,
+            np.dtype(np.uint64): KEY_U64, np.dtype(np.int64): KEY_I64,
+            np.dtype(np.float32): KEY_F32, np.dtype(np.float64): KEY_F64}
+
+SRS_OK = 0
+
+
+class SrsError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    """The HIP library; raises if it has not been built (no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"libsrs_amd.so not built: {LIB_PATH} (run `make -C simd-radix-sort_amd`)")
+    L = ctypes.CDLL(LIB_PATH)
+    i64, i32, u32, vp = ctypes.c_int64, ctypes.c_int32, ctypes.c_uint32, ctypes.c_void_p
+    L.srs_sort_soa.argtypes = [i64, ctypes.c_int, ctypes.c_int, i64, vp, i32, vp, vp]
+    L.srs_sort_aos.argtypes = [i64, ctypes.c_int, ctypes.c_int, i64, vp, u32]
+    L.srs_sort_soa_device.argtypes = [i64, ctypes.c_int, ctypes.c_int, i64, vp, i32, vp, vp,
+                                      vp, vp, vp]
+    L.srs_sort_aos_device.argtypes = [i64, ctypes.c_int, ctypes.c_int, i64, vp, u32, vp, vp]
+    L.srs_fill_synthetic_device.argtypes = [i64, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64,
+                                            vp, i32, vp, vp, vp]
+    L.srs_last_error.restype = ctypes.c_char_p
+    L.srs_version.restype = ctypes.c_char_p
+    L.srs_set_kernel_timing.argtypes = [ctypes.c_int]
+    L.srs_kernel_stats.argtypes = [ctypes.c_char_p, ctypes.POINTER(i64),
+                                   ctypes.POINTER(ctypes.c_double),
+                                   ctypes.POINTER(ctypes.c_double)]
+    _lib = L
+    return L
+
+
+def _check(rc: int):
+    if rc != SRS_OK:
+        raise SrsError(f"srs error {rc}: {lib().srs_last_error().decode()}")
+
+
+def version() -> str:
+    return lib().srs_version().decode()
+
+
+def key_kind_of(dtype) -> int:
+    dt = np.dtype(dtype)
+    if dt not in _NP_KIND:
+        raise TypeError(f"unsupported key dtype {dt}")
+    return _NP_KIND[dt]
+
+
+def _ptr_array(ptrs):
+    return (ctypes.c_void_p * max(1, len(ptrs)))(*ptrs)
+
+
+def _size_array(sizes):
+    return (ctypes.c_uint32 * max(1, len(sizes)))(*sizes)
+
+
+# --------------------------------------------------------------------------
+# host arrays (drop-in semantics: in place, synchronous)
+# --------------------------------------------------------------------------
+def sort_thresh(cmp_sort_threshold: int, keys: np.ndarray, *payloads: np.ndarray,
+                up: bool = True) -> None:
+    """radix_sort::sort<Up, BitSorterSIMD, CmpSorterInsertionSort>(thresh, num,
+    keys, payloads...) on host numpy arrays, in place."""
+    n = len(keys)
+    for a in (keys,) + payloads:
+        if not (isinstance(a, np.ndarray) and a.flags.c_contiguous and a.ndim == 1):
+            raise ValueError("arrays must be 1-D C-contiguous numpy arrays")
+        if len(a) != n:
+            raise ValueError("all arrays must have the same length")
+    _check(lib().srs_sort_soa(n, key_kind_of(keys.dtype), int(bool(up)), int(cmp_sort_threshold),
+                              keys.ctypes.data, len(payloads),
+                              _ptr_array([p.ctypes.data for p in payloads]),
+                              _size_array([p.dtype.itemsize for p in payloads])))
+
+
+def sort(keys: np.ndarray, *payloads: np.ndarray, up: bool = True) -> None:
+    """radix_sort::sort<Up>(num, keys, payloads...) (radixSort.hpp:1780): threshold 16."""
+    sort_thresh(16, keys, *payloads, up=up)
+
+
+def sort_combined(elements: np.ndarray, key_kind: int, up: bool = True,
+                  cmp_sort_threshold: int = 16) -> None:
+    """radix_sort::sort(num, (DataElement<K, Ps...>*) combined): `elements` is a
+    C-contiguous array whose rows are records (2-D uint8 (n, elem_size), or a
+    structured / plain 1-D array); the key of kind `key_kind` is at byte 0."""
+    if not elements.flags.c_contiguous:
+        raise ValueError("elements must be C-contiguous")
+    n = elements.shape[0]
+    esz = elements.nbytes // n if n else elements.dtype.itemsize
+    _check(lib().srs_sort_aos(n, int(key_kind), int(bool(up)), int(cmp_sort_threshold),
+                              elements.ctypes.data, esz))
+
+
+# --------------------------------------------------------------------------
+# device tensors (torch, already in HBM; asynchronous on the current stream)
+# --------------------------------------------------------------------------
+_TORCH_KIND = None
+
+
+def _torch_kind(t) -> int:
+    global _TORCH_KIND
+    import torch
+    if _TORCH_KIND is None:
+        _TORCH_KIND = {torch.uint8: KEY_U8, torch.int8: KEY_I8, torch.int16: KEY_I16,
+                       torch.int32: KEY_I32, torch.int64: KEY_I64, torch.float32: KEY_F32,
+                       torch.float64: KEY_F64}
+        for name, k in (("uint16", KEY_U16), ("uint32", KEY_U32), ("uint64", KEY_U64)):
+            if hasattr(torch, name):
+                _TORCH_KIND[getattr(torch, name)] = k
+    if t.dtype not in _TORCH_KIND:
+        raise TypeError(f"unsupported key dtype {t.dtype}")
+    return _TORCH_KIND[t.dtype]
+
+
+def _stream_ptr(stream=None) -> int:
+    import torch
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return s.cuda_stream
+
+
+def sort_device(keys, *payloads, up: bool = True, cmp_sort_threshold: int = 16,
+                key_kind: int | None = None, out=None, stream=None) -> None:
+    """Sort device tensors. In place unless `out` = (keys_out, *payloads_out).
+    `key_kind` overrides the kind derived from keys.dtype (e.g. torch.int64
+    storage holding uint64 keys)."""
+    for t in (keys,) + payloads:
+        if not (t.is_cuda and t.is_contiguous() and t.dim() == 1 and t.numel() == keys.numel()):
+            raise ValueError("tensors must be 1-D contiguous device tensors of equal length")
+    kind = _torch_kind(keys) if key_kind is None else int(key_kind)
+    np_ = len(payloads)
+    pays = _ptr_array([p.data_ptr() for p in payloads])
+    sizes = _size_array([p.element_size() for p in payloads])
+    if out is not None:
+        if len(out) != 1 + np_:
+            raise ValueError("out must hold keys_out followed by every payload_out")
+        kout = out[0].data_ptr()
+        pout = _ptr_array([o.data_ptr() for o in out[1:]])
+    else:
+        kout, pout = None, None
+    _check(lib().srs_sort_soa_device(keys.numel(), kind, int(bool(up)), int(cmp_sort_threshold),
+                                     keys.data_ptr(), np_, pays, sizes, kout, pout,
+                                     _stream_ptr(stream)))
+
+
+def sort_combined_device(elements, key_kind: int, up: bool = True,
+                         cmp_sort_threshold: int = 16, out=None, stream=None) -> None:
+    """DataElement array on the device: `elements` is a contiguous (n, elem_size)
+    uint8 tensor (or any contiguous tensor whose first dim is the record)."""
+    n = elements.shape[0]
+    esz = elements.numel() * elements.element_size() // max(1, n)
+    _check(lib().srs_sort_aos_device(n, int(key_kind), int(bool(up)), int(cmp_sort_threshold),
+                                     elements.data_ptr(), esz,
+                                     None if out is None else out.data_ptr(),
+                                     _stream_ptr(stream)))
+
+
+def fill_synthetic_device(keys, *payloads, seed: int = 42 << 32, first_index: int = 0,
+                          key_kind: int | None = None, stream=None) -> None:
+    """keys[i] = splitmix64(seed + first_index + i) (see srs_c_api.h);
+    payloads are functions of the key."""
+    kind = _torch_kind(keys) if key_kind is None else int(key_kind)
+    _check(lib().srs_fill_synthetic_device(keys.numel(), kind, seed, first_index,
+                                           keys.data_ptr(), len(payloads),
+                                           _ptr_array([p.data_ptr() for p in payloads]),
+                                           _size_array([p.element_size() for p in payloads]),
+                                           _stream_ptr(stream)))
+
+
+# --------------------------------------------------------------------------
+# kernel timing (HIP events around every launch, see srs_c_api.h)
+# --------------------------------------------------------------------------
+def set_kernel_timing(enable: bool) -> None:
+    _check(lib().srs_set_kernel_timing(int(bool(enable))))
+
+
+def reset_kernel_stats() -> None:
+    _check(lib().srs_reset_kernel_stats())
+
+
+def kernel_stats(name: str):
+    """(launches, total_ms, elements) for a kernel family since the last reset."""
+    n = ctypes.c_int64()
+    ms = ctypes.c_double()
+    el = ctypes.c_double()
+    _check(lib().srs_kernel_stats(name.encode(), ctypes.byref(n), ctypes.byref(ms),
+                                  ctypes.byref(el)))
+    return n.value, ms.value, el.value
+
+
+def release_workspace() -> None:
+    _check(lib().srs_release_workspace())

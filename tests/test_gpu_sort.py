@@ -1,0 +1,268 @@
+"""GPU parity tests: the HIP path (through the C ABI) against the golden
+vectors made by the reference, the CPU oracle, and a stable numpy reference.
+
+Parity contract:
+  * keys: bit-identical to the reference;
+  * payloads: bit-identical whenever payload = f(key) (the reference's own
+    test convention, src/data.hpp:393-406); otherwise the multiset of payload
+    tuples per run of equal keys is identical, and the GPU output equals a
+    STABLE sort bit for bit (the GPU sort is stable, the reference is not);
+  * n <= cmpSortThreshold: bit-identical including payload order (the
+    reference sorts such inputs with its stable insertion sort).
+"""
+import numpy as np
+import pytest
+
+from srs_testlib import (KIND_DTYPES, KIND_NAMES, KIND_UINT, golden_arrays,
+                         golden_manifest, key_size, oracle_sort_aos, oracle_sort_soa,
+                         runs_multiset_equal, stable_reference, transformed_keys)
+
+pytestmark = pytest.mark.gpu
+
+srs_amd = pytest.importorskip("srs_amd")
+
+
+def _torch():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    _torch()
+    srs_amd.lib()
+
+
+def bytes_equal(a, b):
+    return np.array_equal(np.ascontiguousarray(a).view(np.uint8),
+                          np.ascontiguousarray(b).view(np.uint8))
+
+
+def stable_aos(kind, up, elems, thresh=16):
+    ks = key_size(kind)
+    keys = np.ascontiguousarray(elems[:, :ks]).view(KIND_DTYPES[kind]).reshape(-1)
+    (rec,) = stable_reference(kind, up, [keys, np.arange(len(keys))], thresh)[1:]
+    return elems[rec]
+
+
+# ---------------------------------------------------------------------------
+# golden vectors (reference output)
+# ---------------------------------------------------------------------------
+def test_golden_all_cases():
+    m = golden_manifest()
+    fails = []
+    for c in m["cases"]:
+        ins, outs = golden_arrays(c)
+        cols = [a.copy() for a in ins]
+        if c["layout"] == "aos":
+            srs_amd.sort_combined(cols[0], c["key_kind"], up=bool(c["up"]),
+                                  cmp_sort_threshold=c["thresh"])
+        else:
+            srs_amd.sort_thresh(c["thresh"], cols[0], *cols[1:], up=bool(c["up"]))
+        f_of_key = c["family"] in ("soa", "aos", "large")
+        small = c["n"] <= c["thresh"]
+        if c["layout"] == "aos":
+            ks = key_size(c["key_kind"])
+            ok = bytes_equal(cols[0][:, :ks], outs[0][:, :ks])
+            if f_of_key or small:
+                ok &= bytes_equal(cols[0], outs[0])
+            else:
+                ok &= bytes_equal(cols[0], stable_aos(c["key_kind"], c["up"], ins[0], c["thresh"]))
+        else:
+            ok = bytes_equal(cols[0], outs[0])
+            if f_of_key or small:
+                ok &= all(bytes_equal(a, b) for a, b in zip(cols[1:], outs[1:]))
+            else:
+                ok &= runs_multiset_equal(cols[0], outs[0], cols[1:], outs[1:])
+                st = stable_reference(c["key_kind"], c["up"], ins, c["thresh"])
+                ok &= all(bytes_equal(a, b) for a, b in zip(cols, st))
+        if not ok:
+            fails.append((c["family"], KIND_NAMES[c["key_kind"]], c["dist"], c["n"], c["up"]))
+    assert not fails, f"{len(fails)} golden cases differ, e.g. {fails[:5]}"
+
+
+# ---------------------------------------------------------------------------
+# synthetic distributions at sizes that take the multi-level paths
+# ---------------------------------------------------------------------------
+def splitmix64(x):
+    x = (x + np.uint64(0x9E3779B97F4A7C15)) & np.uint64(0xFFFFFFFFFFFFFFFF)
+    x = (x ^ (x >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+    x = (x ^ (x >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return x ^ (x >> np.uint64(31))
+
+
+def make_keys(kind, dist, n, seed):
+    rng = np.random.default_rng(seed)
+    dt = KIND_DTYPES[kind]
+    ut = KIND_UINT[kind]
+    nb = 8 * key_size(kind)
+    if dist == "uniform":
+        if KIND_NAMES[kind].startswith("f"):
+            return rng.uniform(-1, 1, n).astype(dt)
+        return rng.integers(0, 2**nb, n, dtype=np.uint64).astype(ut).view(dt)
+    if dist == "gaussian":
+        if KIND_NAMES[kind].startswith("f"):
+            return rng.normal(0, 1, n).astype(dt)
+        v = np.round(rng.normal(0, 100, n)).astype(np.int64)
+        return v.astype(dt) if KIND_NAMES[kind].startswith("i") else v.astype(ut).view(dt)
+    if dist == "zero":
+        return np.zeros(n, dt)
+    if dist == "zeroone":
+        return rng.integers(0, 2, n).astype(dt)
+    if dist == "sorted":
+        return np.sort(make_keys(kind, "uniform", n, seed))
+    if dist == "reverse":
+        return np.sort(make_keys(kind, "uniform", n, seed))[::-1].copy()
+    if dist == "fewdistinct":
+        vals = make_keys(kind, "uniform", 37, seed + 1)
+        return vals[rng.integers(0, 37, n)]
+    if dist == "highbits":  # only the top byte varies: deep recursion
+        u = rng.integers(0, 256, n, dtype=np.uint64) << np.uint64(nb - 8)
+        return u.astype(ut).view(dt)
+    if dist == "lowbits":  # only the low byte varies: skipped empty levels
+        return rng.integers(0, 256, n, dtype=np.uint64).astype(ut).view(dt)
+    raise ValueError(dist)
+
+
+def payload_of(keys, size, salt=0):
+    bits = keys.view(KIND_UINT[list(map(np.dtype, KIND_DTYPES)).index(keys.dtype)]).astype(np.uint64)
+    h = splitmix64(bits ^ np.uint64(salt * 0x9E37))
+    return h.astype({1: np.uint8, 2: np.uint16, 4: np.uint32, 8: np.uint64}[size])
+
+
+DISTS = ["uniform", "gaussian", "zero", "zeroone", "sorted", "reverse", "fewdistinct",
+         "highbits", "lowbits"]
+
+
+@pytest.mark.parametrize("kind", range(10), ids=KIND_NAMES)
+@pytest.mark.parametrize("up", [True, False], ids=["up", "down"])
+def test_distributions_vs_stable_and_oracle(kind, up):
+    for di, dist in enumerate(DISTS):
+        for n in (9000, 70001):
+            keys = make_keys(kind, dist, n, 1000 * kind + 10 * di + n % 7)
+            p64 = payload_of(keys, 8)
+            idx = np.arange(n, dtype=np.uint32)  # NOT a function of the key
+            k, a, b = keys.copy(), p64.copy(), idx.copy()
+            srs_amd.sort(k, a, b, up=up)
+            st = stable_reference(kind, up, [keys, p64, idx])
+            assert bytes_equal(k, st[0]), (dist, n, "keys")
+            assert bytes_equal(a, st[1]), (dist, n, "f(key) payload")
+            assert bytes_equal(b, st[2]), (dist, n, "index payload (stability)")
+            if n == 9000:  # the oracle restates the reference's own algorithm
+                ok, op = keys.copy(), p64.copy()
+                oracle_sort_soa(kind, up, ok, [op])
+                assert bytes_equal(k, ok) and bytes_equal(a, op), (dist, n, "oracle")
+
+
+@pytest.mark.parametrize("n", [0, 1, 2, 3, 15, 16, 17, 63, 64, 65, 4095, 4096, 8191, 8192,
+                               8193, 12287, 16384, 16385, 24577, 100003, 1 << 20])
+def test_sizes_u64_vs_oracle(n):
+    keys = make_keys(6, "uniform", n, n)
+    pay = payload_of(keys, 8)
+    k, p = keys.copy(), pay.copy()
+    srs_amd.sort(k, p)
+    ok, op = keys.copy(), pay.copy()
+    oracle_sort_soa(6, True, ok, [op])
+    assert bytes_equal(k, ok) and bytes_equal(p, op)
+
+
+@pytest.mark.parametrize("sizes", [[1], [2], [4], [8], [8, 1], [4, 4], [8, 8, 8], [1] * 63,
+                                   [2, 8, 1, 4]])
+def test_payload_packs(sizes):
+    n = 50000
+    keys = make_keys(5, "gaussian", n, 7)
+    pays = [payload_of(keys, s, salt=i) for i, s in enumerate(sizes)]
+    idx = np.arange(n, dtype=np.uint64)
+    cols = [keys.copy()] + [p.copy() for p in pays] + [idx.copy()]
+    srs_amd.sort(*cols)
+    st = stable_reference(5, True, [keys] + pays + [idx])
+    assert all(bytes_equal(a, b) for a, b in zip(cols, st))
+
+
+@pytest.mark.parametrize("kind", [0, 3, 4, 6, 8, 9], ids=lambda k: KIND_NAMES[k])
+@pytest.mark.parametrize("esz_mult", [1, 2, 4, 8])
+@pytest.mark.parametrize("up", [True, False], ids=["up", "down"])
+def test_combined_records(kind, esz_mult, up):
+    ks = key_size(kind)
+    esz = ks * esz_mult
+    if esz > 64:
+        pytest.skip("DataElement larger than 64 bytes")
+    n = 30011
+    keys = make_keys(kind, "gaussian" if kind in (3, 8) else "uniform", n, esz)
+    rng = np.random.default_rng(esz)
+    elems = rng.integers(0, 256, (n, esz), dtype=np.uint8)
+    elems[:, :ks] = keys.view(np.uint8).reshape(n, ks)
+    e = elems.copy()
+    srs_amd.sort_combined(e, kind, up=up)
+    assert bytes_equal(e, stable_aos(kind, up, elems))
+    if n < 40000:
+        o = elems.copy()
+        oracle_sort_aos(kind, up, o)
+        assert bytes_equal(e[:, :ks], o[:, :ks])
+
+
+# ---------------------------------------------------------------------------
+# device API (torch tensors in HBM)
+# ---------------------------------------------------------------------------
+def test_device_inplace_and_out_of_place():
+    torch = _torch()
+    n = 3_000_000
+    dev = torch.device("cuda:0")
+    keys = torch.empty(n, dtype=torch.int64, device=dev)
+    p0 = torch.empty(n, dtype=torch.int32, device=dev)
+    p1 = torch.empty(n, dtype=torch.int32, device=dev)
+    srs_amd.fill_synthetic_device(keys, p0, p1, key_kind=srs_amd.KEY_U64)
+    k_in = keys.clone()
+    p0_in, p1_in = p0.clone(), p1.clone()
+    ko, o0, o1 = torch.empty_like(keys), torch.empty_like(p0), torch.empty_like(p1)
+    srs_amd.sort_device(keys, p0, p1, key_kind=srs_amd.KEY_U64, out=(ko, o0, o1))
+    torch.cuda.synchronize()
+    assert torch.equal(keys, k_in) and torch.equal(p0, p0_in) and torch.equal(p1, p1_in)
+    srs_amd.sort_device(keys, p0, p1, key_kind=srs_amd.KEY_U64)
+    torch.cuda.synchronize()
+    assert torch.equal(keys, ko) and torch.equal(p0, o0) and torch.equal(p1, o1)
+    kh = k_in.cpu().numpy().view(np.uint64)
+    st = stable_reference(6, True, [kh, p0_in.cpu().numpy(), p1_in.cpu().numpy()])
+    assert bytes_equal(ko.cpu().numpy(), st[0])
+    assert bytes_equal(o0.cpu().numpy(), st[1]) and bytes_equal(o1.cpu().numpy(), st[2])
+
+
+def test_device_float_keys_two_payloads():
+    """C2 shape: f32 keys in [-1, 1) + two u32 payload columns."""
+    torch = _torch()
+    n = 2_000_003
+    dev = torch.device("cuda:0")
+    keys = torch.empty(n, dtype=torch.float32, device=dev)
+    p0 = torch.empty(n, dtype=torch.int32, device=dev)
+    p1 = torch.empty(n, dtype=torch.int32, device=dev)
+    srs_amd.fill_synthetic_device(keys, p0, p1)
+    kh, ah, bh = keys.cpu().numpy(), p0.cpu().numpy(), p1.cpu().numpy()
+    srs_amd.sort_device(keys, p0, p1)
+    torch.cuda.synchronize()
+    st = stable_reference(8, True, [kh, ah, bh])
+    assert bytes_equal(keys.cpu().numpy(), st[0])
+    assert bytes_equal(p0.cpu().numpy(), st[1]) and bytes_equal(p1.cpu().numpy(), st[2])
+
+
+def test_device_combined_records():
+    """C3 shape: DataElement<uint64, uint64> records."""
+    torch = _torch()
+    n = 2_000_000
+    dev = torch.device("cuda:0")
+    keys = torch.empty(n, dtype=torch.int64, device=dev)
+    pays = torch.empty(n, dtype=torch.int64, device=dev)
+    srs_amd.fill_synthetic_device(keys, pays, key_kind=srs_amd.KEY_U64)
+    rec = torch.stack([keys, pays], dim=1).contiguous()
+    host = rec.cpu().numpy().view(np.uint8).reshape(n, 16).copy()
+    srs_amd.sort_combined_device(rec, srs_amd.KEY_U64)
+    torch.cuda.synchronize()
+    assert bytes_equal(rec.cpu().numpy().view(np.uint8).reshape(n, 16), stable_aos(6, True, host))
+
+
+def test_errors_are_loud():
+    with pytest.raises(srs_amd.SrsError):
+        srs_amd.sort_combined(np.zeros((10, 12), np.uint8), srs_amd.KEY_U32)  # not a power of two
+    with pytest.raises(TypeError):
+        srs_amd.sort(np.zeros(10, np.complex64))
