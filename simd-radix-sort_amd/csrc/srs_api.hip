@@ -173,9 +173,9 @@ struct Workspace {
   DevBuf tmp;         // TMP data buffer (same footprint as the input)
   DevBuf stage;       // device copy of host arrays (host-pointer API)
   DevBuf desc;        // SortDesc
-  DevBuf big[2], local, copy;
-  DevBuf plan, tcount, hcount, tbase, hbase, var;
-  DevBuf tile_seg, hist, scan_tmp, totals, ctr;
+  DevBuf big[2], local, local2, copy, fallback;
+  DevBuf plan, tcount, gcount, tbase, gbase, var, sbase;
+  DevBuf tile_seg, group_seg, hist, offs, gsum, gofs, scan_tmp, totals, ctr;
   ListCounters* h_ctr = nullptr;
   uint64_t* h_totals = nullptr;
 };
@@ -283,7 +283,6 @@ int run_sort(Workspace* W, const Request& R, hipStream_t st) {
       d.cols[nc++] = Col{{in + off, out + off, tmp + off}, slice, E};
     }
     d.ncols = nc;
-    d.col0_is_key = 0;
   } else {
     for (int c = 0; c < R.ncols; c++) {
       d.cols[c] = Col{{(char*)R.in_cols[c], (char*)R.out_cols[c], tmp + tmp_off[c]},
@@ -291,7 +290,6 @@ int run_sort(Workspace* W, const Request& R, hipStream_t st) {
     }
     d.key = d.cols[0];
     d.ncols = R.ncols;
-    d.col0_is_key = 1;
   }
   if (inplace)  // IN aliases OUT: a segment that never moved is already home
     for (int c = 0; c < d.ncols; c++) d.cols[c].base[BUF_IN] = d.cols[c].base[BUF_OUT];
@@ -307,26 +305,32 @@ int run_sort(Workspace* W, const Request& R, hipStream_t st) {
   SRS_TRY(ensure(W->big[0], big_cap * sizeof(Seg)));
   SRS_TRY(ensure(W->big[1], big_cap * sizeof(Seg)));
   SRS_TRY(ensure(W->local, local_cap * sizeof(Seg)));
+  SRS_TRY(ensure(W->local2, local_cap * sizeof(Seg)));
   SRS_TRY(ensure(W->copy, copy_cap * sizeof(Seg)));
   SRS_TRY(ensure(W->ctr, sizeof(ListCounters)));
   SRS_TRY(ensure(W->totals, 4 * sizeof(uint64_t)));
   ListCounters* d_ctr = (ListCounters*)W->ctr.p;
   uint64_t* d_totals = (uint64_t*)W->totals.p;
-  launch_init_lists(seg0, to_local ? 1 : 0, (Seg*)W->big[0].p, (Seg*)W->local.p, d_ctr, st);
+  launch_init_lists(seg0, to_local ? 1 : 0, (Seg*)W->big[0].p, (Seg*)W->local.p,
+                    (Seg*)W->local2.p, d_ctr, st);
 
   int64_t nbig = to_local ? 0 : 1;
-  int64_t n_local = to_local ? 1 : 0, n_copy = 0;
+  int64_t n_local = (to_local && n <= kLocalCapSmall) ? 1 : 0;
+  int64_t n_local2 = (to_local && n > kLocalCapSmall) ? 1 : 0;
+  int64_t n_copy = 0;
+  W->h_ctr->local_elems = to_local ? (uint64_t)n : 0;
   int cur = 0;
   int level = 0;
   while (nbig > 0) {
     if (++level > 80) return fail(SRS_ERR_INTERNAL, "level limit exceeded");
-    // ---- plan + tile / histogram bases
+    // ---- plan + tile / scan-group bases
     SRS_TRY(ensure(W->plan, nbig * sizeof(SegPlan)));
     SRS_TRY(ensure(W->tcount, nbig * 8));
-    SRS_TRY(ensure(W->hcount, nbig * 8));
+    SRS_TRY(ensure(W->gcount, nbig * 8));
     SRS_TRY(ensure(W->tbase, nbig * 8));
-    SRS_TRY(ensure(W->hbase, nbig * 8));
+    SRS_TRY(ensure(W->gbase, nbig * 8));
     SRS_TRY(ensure(W->var, nbig * 8));
+    SRS_TRY(ensure(W->sbase, (size_t)nbig * kMaxBins * 8));
     SRS_TRY(ensure(W->scan_tmp, scan_temp_elems(nbig) * 8));
     SegPlan* plan = (SegPlan*)W->plan.p;
     unsigned long long* var = (unsigned long long*)W->var.p;
@@ -334,64 +338,73 @@ int run_sort(Workspace* W, const Request& R, hipStream_t st) {
       TimedScope ts("plan", (double)nbig, st);
       HIP_TRY(hipMemsetAsync(d_totals + 3, 0, sizeof(uint64_t), st));
       launch_plan((Seg*)W->big[cur].p, nbig, plan, (int64_t*)W->tcount.p,
-                  (int64_t*)W->hcount.p, var, d_totals + 3, st);
+                  (int64_t*)W->gcount.p, var, d_totals + 3, st);
       launch_excl_scan((uint64_t*)W->tcount.p, (uint64_t*)W->tbase.p, nbig,
                        (uint64_t*)W->scan_tmp.p, d_totals + 0, st);
-      launch_excl_scan((uint64_t*)W->hcount.p, (uint64_t*)W->hbase.p, nbig,
+      launch_excl_scan((uint64_t*)W->gcount.p, (uint64_t*)W->gbase.p, nbig,
                        (uint64_t*)W->scan_tmp.p, d_totals + 1, st);
-      launch_plan_bases(plan, nbig, (int64_t*)W->tbase.p, (int64_t*)W->hbase.p, st);
+      launch_plan_bases(plan, nbig, (int64_t*)W->tbase.p, (int64_t*)W->gbase.p, st);
     }
     HIP_TRY(hipMemcpyAsync(W->h_totals, d_totals, 4 * sizeof(uint64_t),
                            hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
     const int64_t ntiles = (int64_t)W->h_totals[0];
-    const int64_t nhist = (int64_t)W->h_totals[1];
+    const int64_t ngroups = (int64_t)W->h_totals[1];
     const double level_elems = (double)W->h_totals[3];
     note_elems("count", level_elems);
     note_elems("scatter", level_elems);
 
     SRS_TRY(ensure(W->tile_seg, ntiles * 4));
-    SRS_TRY(ensure(W->hist, nhist * 8));
-    SRS_TRY(ensure(W->scan_tmp, scan_temp_elems(std::max(nhist, nbig)) * 8));
+    SRS_TRY(ensure(W->group_seg, ngroups * 4));
+    SRS_TRY(ensure(W->hist, (size_t)ntiles * kMaxBins * 4));
+    SRS_TRY(ensure(W->offs, (size_t)ntiles * kMaxBins * 8));
+    SRS_TRY(ensure(W->gsum, (size_t)ngroups * kMaxBins * 4));
+    SRS_TRY(ensure(W->gofs, (size_t)ngroups * kMaxBins * 8));
     int32_t* tile_seg = (int32_t*)W->tile_seg.p;
-    uint64_t* hist = (uint64_t*)W->hist.p;
-    launch_tile_map(plan, nbig, ntiles, tile_seg, st);
+    int32_t* group_seg = (int32_t*)W->group_seg.p;
+    launch_seg_map((int64_t*)W->tbase.p, nbig, ntiles, tile_seg, st);
+    launch_seg_map((int64_t*)W->gbase.p, nbig, ngroups, group_seg, st);
     {
       TimedScope ts("count", (double)0, st);
-      launch_count(ks, d_desc, plan, tile_seg, ntiles, hist, var, st);
+      launch_count(ks, d_desc, plan, tile_seg, ntiles, (uint32_t*)W->hist.p, var, st);
     }
-    {
-      TimedScope ts("scan", (double)nhist, st);
-      launch_excl_scan(hist, hist, nhist, (uint64_t*)W->scan_tmp.p, d_totals + 2, st);
-    }
-    // ---- children (list capacity for the worst case: every bin non-empty)
+    // ---- offsets + children (list capacity for the worst case: every bin non-empty)
     const size_t worst = (size_t)nbig * kMaxBins;
     const int nxt = cur ^ 1;
     SRS_TRY(ensure(W->big[nxt], worst * sizeof(Seg)));
     SRS_TRY(ensure_keep(W->local, (n_local + worst) * sizeof(Seg), n_local * sizeof(Seg), st));
+    SRS_TRY(ensure_keep(W->local2, (n_local2 + worst) * sizeof(Seg), n_local2 * sizeof(Seg), st));
     SRS_TRY(ensure_keep(W->copy, (n_copy + worst) * sizeof(Seg), n_copy * sizeof(Seg), st));
     HIP_TRY(hipMemsetAsync(&d_ctr->n_big, 0, sizeof(unsigned long long), st));
     {
-      TimedScope ts("children", (double)nbig, st);
-      launch_children(plan, nbig, hist, var, (Seg*)W->big[nxt].p, (Seg*)W->local.p,
-                      (Seg*)W->copy.p, d_ctr, st);
+      TimedScope ts("scan", (double)ntiles, st);
+      launch_offsets(plan, nbig, group_seg, ngroups, (uint32_t*)W->hist.p,
+                     (uint32_t*)W->gsum.p, (uint64_t*)W->gofs.p, (uint64_t*)W->sbase.p,
+                     (uint64_t*)W->offs.p, var, (Seg*)W->big[nxt].p, (Seg*)W->local.p,
+                     (Seg*)W->local2.p, (Seg*)W->copy.p, d_ctr, st);
     }
     {
       TimedScope ts("scatter", (double)0, st);
-      launch_scatter(ks, d_desc, plan, tile_seg, hist, ntiles, st);
+      launch_scatter(ks, d_desc, plan, tile_seg, (uint64_t*)W->offs.p, ntiles, st);
     }
     HIP_TRY(hipMemcpyAsync(W->h_ctr, d_ctr, sizeof(ListCounters), hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
     nbig = (int64_t)W->h_ctr->n_big;
     n_local = (int64_t)W->h_ctr->n_local;
+    n_local2 = (int64_t)W->h_ctr->n_local2;
     n_copy = (int64_t)W->h_ctr->n_copy;
     cur = nxt;
   }
 
-  if (n_local > 0) {
+  if (n_local + n_local2 > 0) {
     note_elems("local", (double)W->h_ctr->local_elems);
     TimedScope ts("local", (double)0, st);
-    launch_local(ks, d_desc, (Seg*)W->local.p, n_local, st);
+    SRS_TRY(ensure(W->fallback, (n_local + n_local2) * sizeof(Seg)));
+    Seg* fb = (Seg*)W->fallback.p;
+    unsigned long long* nfb = &d_ctr->n_fallback;
+    if (n_local2 > 0) launch_local(ks, d_desc, (Seg*)W->local2.p, n_local2, 1, fb, nfb, st);
+    if (n_local > 0) launch_local(ks, d_desc, (Seg*)W->local.p, n_local, 0, fb, nfb, st);
+    launch_local_lsd(ks, d_desc, fb, nfb, (int)std::min<int64_t>(1024, n_local + n_local2), st);
   }
   if (n_copy > 0) {
     std::vector<Seg> cp((size_t)n_copy);
@@ -636,9 +649,10 @@ int srs_release_workspace(void) {
   std::lock_guard<std::mutex> lk(g_wmu);
   for (auto& kv : g_ws) {
     Workspace* w = kv.second;
-    DevBuf* bufs[] = {&w->tmp, &w->stage, &w->desc, &w->big[0], &w->big[1], &w->local,
-                      &w->copy, &w->plan, &w->tcount, &w->hcount, &w->tbase, &w->hbase,
-                      &w->var, &w->tile_seg, &w->hist, &w->scan_tmp, &w->totals, &w->ctr};
+    DevBuf* bufs[] = {&w->tmp, &w->stage, &w->desc, &w->big[0], &w->big[1], &w->local, &w->local2, &w->fallback,
+                      &w->copy, &w->plan, &w->tcount, &w->gcount, &w->tbase, &w->gbase,
+                      &w->var, &w->sbase, &w->tile_seg, &w->group_seg, &w->hist, &w->offs,
+                      &w->gsum, &w->gofs, &w->scan_tmp, &w->totals, &w->ctr};
     for (DevBuf* b : bufs)
       if (b->p) (void)hipFree(b->p);
     (void)hipHostFree(w->h_ctr);

@@ -33,9 +33,9 @@ struct Col {
 // Everything a kernel needs to read keys and move records.
 struct SortDesc {
   Col key;                 // key view (width = key size)
-  Col cols[SRS_MAX_COLS];  // columns moved with every key
+  Col cols[SRS_MAX_COLS];  // columns moved with every key; cols[0] holds the
+                           // key in its low bytes (SoA key column / AoS slice 0)
   int32_t ncols;
-  int32_t col0_is_key;     // SoA: cols[0] is the key column (moved from registers)
   int32_t key_bits;        // 8 * key size
   int32_t canon_zero;      // float keys, n <= cmpSortThreshold: -0.0 == +0.0
   // transformed key u = bits ^ (bits & signbit ? mneg : mpos)
@@ -54,8 +54,9 @@ struct SegPlan {
   int64_t start;
   int64_t len;
   int64_t tile_base;  // first tile of this segment in the level's tile space
-  int64_t hist_base;  // first histogram entry (bin-major: bin * ntiles + tile)
+  int64_t group_base; // first scan group (kScanGroup tiles) of this segment
   int32_t ntiles;
+  int32_t ngroups;
   int32_t shift;      // digit = (u >> shift) & ((1 << bits) - 1)
   int32_t bits;
   int32_t buf;        // source buffer
@@ -68,19 +69,24 @@ struct ListCounters {
   unsigned long long n_big;    // segments for the next global level
   unsigned long long n_local;  // segments for the LDS sort
   unsigned long long n_copy;   // finished segments that must be copied to OUT
-  unsigned long long local_elems;  // keys in the local list (timing stats)
+  unsigned long long local_elems;  // keys in the local lists (timing stats)
+  unsigned long long n_local2; // segments for the large-class LDS sort
+  unsigned long long n_fallback;  // segments handed to the LSD fallback kernel
 };
 
 // Tuning constants (see DESIGN.md §4 for how they were chosen).
 constexpr int kScatterThreads = 512;
-constexpr int kScatterItems = 16;
-constexpr int kTile = kScatterThreads * kScatterItems;   // 8192 keys per tile
-constexpr int kMaxDigitBits = 10;
-constexpr int kMaxBins = 1 << kMaxDigitBits;
+constexpr int kScatterItems = 12;
+constexpr int kTile = kScatterThreads * kScatterItems;   // 6144 keys per tile
+constexpr int kMaxDigitBits = 9;
+constexpr int kMaxBins = 1 << kMaxDigitBits;   // histogram row stride (tile-major)
+constexpr int kScanGroup = 256;                 // tiles per column-scan group
 
-constexpr int kLocalThreads = 512;
 constexpr int kLocalItems = 16;
+constexpr int kLocalThreads = 512;
 constexpr int kLocalCap = kLocalThreads * kLocalItems;    // 8192 keys per segment
+constexpr int kLocalThreadsSmall = 256;
+constexpr int kLocalCapSmall = kLocalThreadsSmall * kLocalItems;  // 4096
 constexpr int kLocalTarget = 6144;                        // digit sizing target
 
 }  // namespace srs

@@ -108,12 +108,70 @@ __device__ __forceinline__ T block_excl_scan(T v, T* sh, T* total) {
   return r;
 }
 
+// Workgroup barrier that orders LDS accesses only. __syncthreads() also waits
+// for every outstanding global load AND store of the wave (s_waitcnt
+// vmcnt(0)); kernels that keep stores or prefetch loads in flight across a
+// barrier use this one instead.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+template <int NT, typename T>
+__device__ __forceinline__ T block_excl_scan_lds(T v, T* sh, T* total) {
+  constexpr int NW = NT / 64;
+  const uint32_t wave = threadIdx.x >> 6;
+  T inc = wave_incl_scan(v);
+  if (lane_id() == 63) sh[wave] = inc;
+  lds_barrier();
+  if (threadIdx.x == 0) {
+    T run = 0;
+#pragma unroll
+    for (int w = 0; w < NW; w++) {
+      T t = sh[w];
+      sh[w] = run;
+      run += t;
+    }
+    sh[NW] = run;
+  }
+  lds_barrier();
+  T r = inc - v + sh[wave];
+  *total = sh[NW];
+  lds_barrier();
+  return r;
+}
+
 // Wave-level multisplit rank (stable): for each item slot k, lanes whose
 // digit matches form a peer group found with `nbits` ballots; the rank of a
 // key is the wave's running count of its digit (per-wave LDS counter row
 // `wc`) plus the number of lower-lane peers. Items are in striped order
 // (slot k of lane l = wave-local element k * 64 + l), so ranks follow input
 // order within a digit.
+template <int ITEMS, typename DigitFn, typename ValidFn>
+__device__ __forceinline__ void wlms_rank_fn(DigitFn digit, ValidFn valid, int nbits,
+                                             uint16_t* wc, uint32_t (&rank)[ITEMS]) {
+  const uint64_t lt = (lane_id() == 0) ? 0ull : (~0ull >> (64 - lane_id()));
+#pragma unroll
+  for (int k = 0; k < ITEMS; k++) {
+    const bool ok = valid(k);
+    uint64_t peers = __ballot(ok);
+    const uint32_t d = digit(k);
+#pragma unroll
+    for (int b = 0; b < kMaxDigitBits; b++) {
+      if (b < nbits) {
+        const bool bit = (d >> b) & 1u;
+        const uint64_t m = __ballot(bit);
+        peers &= bit ? m : ~m;
+      }
+    }
+    if (ok) {
+      const uint32_t below = (uint32_t)__popcll(peers & lt);
+      const uint32_t base = wc[d];
+      rank[k] = base + below;
+      if (below == 0) wc[d] = (uint16_t)(base + (uint32_t)__popcll(peers));
+    }
+  }
+}
+
 template <int ITEMS>
 __device__ __forceinline__ void wlms_rank(const uint32_t (&dig)[ITEMS],
                                           const bool (&valid)[ITEMS], int nbits,
@@ -147,10 +205,21 @@ __device__ __forceinline__ void wlms_rank(const uint32_t (&dig)[ITEMS],
 // Digit width for a segment of `len` keys with `rbits` unsorted bits: as many
 // bits as needed to bring buckets under kLocalTarget, spread evenly over the
 // levels that will take, at most kMaxDigitBits per level.
-__device__ __forceinline__ int choose_bits(int64_t len, int rbits) {
+__device__ __forceinline__ int levels_for(int64_t len, int64_t target, int* need_out) {
   int need = 1;
-  while (need < 62 && ((int64_t)kLocalTarget << need) < len) need++;
-  const int levels = (need + kMaxDigitBits - 1) / kMaxDigitBits;
+  while (need < 62 && (target << need) < len) need++;
+  *need_out = need;
+  return (need + kMaxDigitBits - 1) / kMaxDigitBits;
+}
+
+__device__ __forceinline__ int choose_bits(int64_t len, int rbits) {
+  // bits needed to bring buckets under kLocalTarget, spread evenly over the
+  // levels that takes (<= kMaxDigitBits each); one more bit when that lands
+  // the buckets in the smaller (faster) LDS class without an extra level
+  int need, need_small;
+  const int levels = levels_for(len, kLocalTarget, &need);
+  const int levels_small = levels_for(len, kLocalTarget / 2, &need_small);
+  if (levels_small == levels) need = need_small;
   int bits = (need + levels - 1) / levels;
   if (bits > kMaxDigitBits) bits = kMaxDigitBits;
   if (bits > rbits) bits = rbits;
@@ -160,7 +229,7 @@ __device__ __forceinline__ int choose_bits(int64_t len, int rbits) {
 
 __global__ void plan_kernel(const Seg* __restrict__ big, int64_t nbig,
                             SegPlan* __restrict__ plan, int64_t* __restrict__ tcount,
-                            int64_t* __restrict__ hcount,
+                            int64_t* __restrict__ gcount,
                             unsigned long long* __restrict__ var_or,
                             uint64_t* __restrict__ elems) {
   const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -173,37 +242,49 @@ __global__ void plan_kernel(const Seg* __restrict__ big, int64_t nbig,
   p.bits = choose_bits(g.len, g.rbits);
   p.shift = g.rbits - p.bits;
   p.ntiles = (int32_t)((g.len + kTile - 1) / kTile);
+  p.ngroups = (p.ntiles + kScanGroup - 1) / kScanGroup;
   p.buf = g.buf;
   p.dst = (g.buf == BUF_TMP) ? BUF_OUT : BUF_TMP;
   p.skip = 0;
   p.tile_base = 0;
-  p.hist_base = 0;
+  p.group_base = 0;
   plan[s] = p;
   tcount[s] = p.ntiles;
-  hcount[s] = (int64_t)p.ntiles << p.bits;
+  gcount[s] = p.ngroups;
   var_or[s] = 0;
 }
 
 __global__ void plan_bases_kernel(SegPlan* __restrict__ plan, int64_t nbig,
                                   const int64_t* __restrict__ tbase,
-                                  const int64_t* __restrict__ hbase) {
+                                  const int64_t* __restrict__ gbase) {
   const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= nbig) return;
   plan[s].tile_base = tbase[s];
-  plan[s].hist_base = hbase[s];
+  plan[s].group_base = gbase[s];
 }
 
-// tile -> segment (binary search over the segments' tile bases).
-__global__ void tile_map_kernel(const SegPlan* __restrict__ plan, int64_t nbig,
-                                int64_t ntiles, int32_t* __restrict__ tile_seg) {
+// index -> segment (binary search over the segments' exclusive bases)
+__global__ void seg_map_kernel(const int64_t* __restrict__ bases, int64_t nbig, int64_t n,
+                               int32_t* __restrict__ out) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= ntiles) return;
+  if (t >= n) return;
   int64_t lo = 0, hi = nbig - 1;
   while (lo < hi) {
     const int64_t mid = (lo + hi + 1) >> 1;
-    if (plan[mid].tile_base <= t) lo = mid; else hi = mid - 1;
+    if (bases[mid] <= t) lo = mid; else hi = mid - 1;
   }
-  tile_seg[t] = (int32_t)lo;
+  out[t] = (int32_t)lo;
+}
+
+// XCD-aware block -> tile map: consecutive tiles run on one XCD (blocks are
+// dealt round-robin over the 8 XCDs), so the partial cache lines that two
+// neighbouring tiles write into the same bucket meet in one L2. Bijective for
+// any grid size. Placement only affects speed, never results.
+__device__ __forceinline__ int64_t xcd_remap(int64_t bid, int64_t nwg) {
+  constexpr int64_t X = 8;
+  const int64_t q = nwg / X, r = nwg % X;
+  const int64_t xcd = bid % X, local = bid / X;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + local;
 }
 
 // ---------------------------------------------------------------------------
@@ -212,11 +293,11 @@ __global__ void tile_map_kernel(const SegPlan* __restrict__ plan, int64_t nbig,
 template <typename KT, typename U>
 __global__ __launch_bounds__(kScatterThreads) void count_kernel(
     const SortDesc* __restrict__ desc, const SegPlan* __restrict__ plan,
-    const int32_t* __restrict__ tile_seg, uint64_t* __restrict__ hist,
+    const int32_t* __restrict__ tile_seg, uint32_t* __restrict__ hist,
     unsigned long long* __restrict__ var_or) {
   __shared__ uint32_t h[kMaxBins];
   __shared__ unsigned long long sh_or;
-  const int64_t t = blockIdx.x;
+  const int64_t t = xcd_remap(blockIdx.x, gridDim.x);
   const int32_t s = tile_seg[t];
   const SegPlan P = plan[s];
   const int64_t tl = t - P.tile_base;
@@ -253,9 +334,41 @@ __global__ __launch_bounds__(kScatterThreads) void count_kernel(
   }
   if (vor) atomicOr(&sh_or, (unsigned long long)vor);
   __syncthreads();
-  for (uint32_t i = threadIdx.x; i < nb; i += kScatterThreads)
-    hist[P.hist_base + (int64_t)i * P.ntiles + tl] = h[i];
-  if (threadIdx.x == 0 && sh_or) atomicOr(&var_or[s], sh_or);
+  // tile-major row: one coalesced 4*nb-byte write per tile
+  uint32_t* row = hist + t * kMaxBins;
+  for (uint32_t i = threadIdx.x; i < nb; i += kScatterThreads) row[i] = h[i];
+  if (threadIdx.x == 0 && sh_or) {
+    // most tiles add no new bits: skip the (contended) atomic then
+    const unsigned long long known =
+        __hip_atomic_load(&var_or[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (sh_or & ~known) atomicOr(&var_or[s], sh_or);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// segmented column scan of the tile-major histograms:
+//   offset(t, b) = sum_{b' < b} total(b') + sum_{t' < t in segment} H[t'][b]
+// in three passes over groups of kScanGroup tiles (all row accesses coalesced)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kMaxBins) void group_sum_kernel(
+    const SegPlan* __restrict__ plan, const int32_t* __restrict__ group_seg,
+    const uint32_t* __restrict__ hist, uint32_t* __restrict__ gsum) {
+  const int64_t g = blockIdx.x;
+  const SegPlan P = plan[group_seg[g]];
+  const uint32_t b = threadIdx.x;
+  if (b >= (1u << P.bits)) return;
+  const int64_t t0 = P.tile_base + (g - P.group_base) * kScanGroup;
+  const int64_t t1 = min(t0 + kScanGroup, P.tile_base + P.ntiles);
+  uint32_t s0 = 0, s1 = 0, s2 = 0, s3 = 0;
+  int64_t t = t0;
+  for (; t + 4 <= t1; t += 4) {
+    s0 += hist[(t + 0) * kMaxBins + b];
+    s1 += hist[(t + 1) * kMaxBins + b];
+    s2 += hist[(t + 2) * kMaxBins + b];
+    s3 += hist[(t + 3) * kMaxBins + b];
+  }
+  for (; t < t1; t++) s0 += hist[t * kMaxBins + b];
+  gsum[g * kMaxBins + b] = s0 + s1 + s2 + s3;
 }
 
 // ---------------------------------------------------------------------------
@@ -324,93 +437,182 @@ __global__ __launch_bounds__(kScanThreads) void scan_apply_kernel(
 // ---------------------------------------------------------------------------
 struct Lists {
   Seg* big;
-  Seg* local;
+  Seg* local;    // segments of <= kLocalCapSmall keys
+  Seg* local2;   // segments of <= kLocalCap keys
   Seg* copy;
   ListCounters* ctr;
 };
+
+__device__ __forceinline__ void emit_local(const Lists& L, const Seg& c) {
+  if (c.len <= kLocalCapSmall) L.local[atomicAdd(&L.ctr->n_local, 1ull)] = c;
+  else L.local2[atomicAdd(&L.ctr->n_local2, 1ull)] = c;
+  atomicAdd(&L.ctr->local_elems, (unsigned long long)c.len);
+}
 
 __device__ __forceinline__ void emit_child(const Lists& L, Seg c) {
   if (c.len <= 0) return;
   if (c.rbits == 0 || c.len == 1) {
     if (c.buf == BUF_OUT) return;  // finished in place
-    if (c.len <= kLocalCap) {
-      L.local[atomicAdd(&L.ctr->n_local, 1ull)] = c;
-      atomicAdd(&L.ctr->local_elems, (unsigned long long)c.len);
-    } else {
-      L.copy[atomicAdd(&L.ctr->n_copy, 1ull)] = c;
-    }
+    if (c.len <= kLocalCap) emit_local(L, c);
+    else L.copy[atomicAdd(&L.ctr->n_copy, 1ull)] = c;
   } else if (c.len <= kLocalCap) {
-    L.local[atomicAdd(&L.ctr->n_local, 1ull)] = c;
-    atomicAdd(&L.ctr->local_elems, (unsigned long long)c.len);
+    emit_local(L, c);
   } else {
     L.big[atomicAdd(&L.ctr->n_big, 1ull)] = c;
   }
 }
 
-__global__ __launch_bounds__(512) void children_kernel(
-    SegPlan* __restrict__ plan, const uint64_t* __restrict__ offs,
-    const unsigned long long* __restrict__ var_or, Seg* big_next, Seg* local,
+// One block per large segment: exclusive scan over its groups (per bin),
+// bin totals, bin bases, and the child segments of the next level.
+// Every thread of the block offers at most one child (c.len == 0: none).
+// Slots are reserved with one global atomic per list per block (a global
+// atomic per child serialises on the counter).
+__device__ __forceinline__ void emit_children_block(const Lists& L, const Seg& c) {
+  enum { C_NONE = -1, C_BIG = 0, C_LOCAL = 1, C_LOCAL2 = 2, C_COPY = 3 };
+  __shared__ unsigned int cnt[4];
+  __shared__ unsigned long long basev[4];
+  __shared__ unsigned long long lsum;
+  int cls = C_NONE;
+  if (c.len > 0) {
+    if (c.rbits == 0 || c.len == 1) {
+      if (c.buf != BUF_OUT)
+        cls = c.len <= kLocalCapSmall ? C_LOCAL : c.len <= kLocalCap ? C_LOCAL2 : C_COPY;
+    } else if (c.len <= kLocalCapSmall) {
+      cls = C_LOCAL;
+    } else if (c.len <= kLocalCap) {
+      cls = C_LOCAL2;
+    } else {
+      cls = C_BIG;
+    }
+  }
+  if (threadIdx.x < 4) cnt[threadIdx.x] = 0;
+  if (threadIdx.x == 0) lsum = 0;
+  __syncthreads();
+  unsigned int my = 0;
+  if (cls != C_NONE) my = atomicAdd(&cnt[cls], 1u);
+  if (cls == C_LOCAL || cls == C_LOCAL2) atomicAdd(&lsum, (unsigned long long)c.len);
+  __syncthreads();
+  if (threadIdx.x == 4 && lsum) atomicAdd(&L.ctr->local_elems, lsum);
+  if (threadIdx.x < 4) {
+    unsigned long long* ctrp = threadIdx.x == C_BIG ? &L.ctr->n_big
+                             : threadIdx.x == C_LOCAL ? &L.ctr->n_local
+                             : threadIdx.x == C_LOCAL2 ? &L.ctr->n_local2 : &L.ctr->n_copy;
+    basev[threadIdx.x] = cnt[threadIdx.x] ? atomicAdd(ctrp, (unsigned long long)cnt[threadIdx.x]) : 0;
+  }
+  __syncthreads();
+  if (cls == C_NONE) return;
+  Seg* list = cls == C_BIG ? L.big : cls == C_LOCAL ? L.local : cls == C_LOCAL2 ? L.local2 : L.copy;
+  list[basev[cls] + my] = c;
+}
+
+__global__ __launch_bounds__(kMaxBins) void seg_scan_kernel(
+    SegPlan* __restrict__ plan, const uint32_t* __restrict__ gsum,
+    uint64_t* __restrict__ gofs, uint64_t* __restrict__ sbase,
+    const unsigned long long* __restrict__ var_or, Seg* big_next, Seg* local, Seg* local2,
     Seg* copy, ListCounters* ctr) {
+  __shared__ uint64_t scan_sh[kMaxBins / 64 + 1];
   __shared__ int single;
   const int64_t s = blockIdx.x;
   const SegPlan P = plan[s];
   const uint32_t nb = 1u << P.bits;
-  const uint64_t seg0 = offs[P.hist_base];
-  if (threadIdx.x == 0) single = 0;
-  __syncthreads();
-  for (uint32_t i = threadIdx.x; i < nb; i += blockDim.x) {
-    const int64_t off = (int64_t)(offs[P.hist_base + (int64_t)i * P.ntiles] - seg0);
-    const int64_t end = (i + 1 < nb)
-        ? (int64_t)(offs[P.hist_base + (int64_t)(i + 1) * P.ntiles] - seg0) : P.len;
-    if (end - off == P.len) single = 1;
+  const uint32_t b = threadIdx.x;
+  if (b == 0) single = 0;
+  uint64_t run = 0;
+  if (b < nb) {
+    const int64_t g0 = P.group_base, g1 = P.group_base + P.ngroups;
+    int64_t g = g0;
+    for (; g + 4 <= g1; g += 4) {
+      const uint32_t a0 = gsum[(g + 0) * kMaxBins + b], a1 = gsum[(g + 1) * kMaxBins + b];
+      const uint32_t a2 = gsum[(g + 2) * kMaxBins + b], a3 = gsum[(g + 3) * kMaxBins + b];
+      gofs[(g + 0) * kMaxBins + b] = run;
+      gofs[(g + 1) * kMaxBins + b] = run + a0;
+      gofs[(g + 2) * kMaxBins + b] = run + a0 + a1;
+      gofs[(g + 3) * kMaxBins + b] = run + a0 + a1 + a2;
+      run += (uint64_t)a0 + a1 + a2 + a3;
+    }
+    for (; g < g1; g++) {
+      gofs[g * kMaxBins + b] = run;
+      run += gsum[g * kMaxBins + b];
+    }
   }
+  uint64_t tot;
+  const uint64_t ex = block_excl_scan<kMaxBins>(run, scan_sh, &tot);
+  if (b < nb) sbase[s * kMaxBins + b] = ex;
+  if (b < nb && (int64_t)run == P.len) single = 1;
   __syncthreads();
-  Lists L{big_next, local, copy, ctr};
+  Seg c;
+  c.len = 0;
   if (single) {
-    if (threadIdx.x == 0) {
+    if (b == 0) {
       plan[s].skip = 1;
       const unsigned long long v = var_or[s];
-      Seg c;
       c.start = P.start;
       c.len = P.len;
       c.rbits = v ? 64 - __clzll((long long)v) : 0;
       if (c.rbits > P.shift) c.rbits = P.shift;  // cannot happen; defensive
       c.buf = P.buf;
-      emit_child(L, c);
     }
-    return;
-  }
-  for (uint32_t i = threadIdx.x; i < nb; i += blockDim.x) {
-    const int64_t off = (int64_t)(offs[P.hist_base + (int64_t)i * P.ntiles] - seg0);
-    const int64_t end = (i + 1 < nb)
-        ? (int64_t)(offs[P.hist_base + (int64_t)(i + 1) * P.ntiles] - seg0) : P.len;
-    Seg c;
-    c.start = P.start + off;
-    c.len = end - off;
+  } else if (b < nb && run > 0) {
+    c.start = P.start + (int64_t)ex;
+    c.len = (int64_t)run;
     c.rbits = P.shift;
     c.buf = P.dst;
-    emit_child(L, c);
+  }
+  emit_children_block(Lists{big_next, local, local2, copy, ctr}, c);
+}
+
+// Per group: turn group offsets into every tile's bucket offsets.
+__global__ __launch_bounds__(kMaxBins) void tile_offs_kernel(
+    const SegPlan* __restrict__ plan, const int32_t* __restrict__ group_seg,
+    const uint32_t* __restrict__ hist, const uint64_t* __restrict__ gofs,
+    const uint64_t* __restrict__ sbase, uint64_t* __restrict__ offs) {
+  const int64_t g = blockIdx.x;
+  const int32_t s = group_seg[g];
+  const SegPlan P = plan[s];
+  const uint32_t b = threadIdx.x;
+  if (P.skip || b >= (1u << P.bits)) return;
+  const int64_t t0 = P.tile_base + (g - P.group_base) * kScanGroup;
+  const int64_t t1 = min(t0 + kScanGroup, P.tile_base + P.ntiles);
+  uint64_t run = sbase[s * kMaxBins + b] + gofs[g * kMaxBins + b];
+  int64_t t = t0;
+  for (; t + 4 <= t1; t += 4) {
+    const uint32_t a0 = hist[(t + 0) * kMaxBins + b], a1 = hist[(t + 1) * kMaxBins + b];
+    const uint32_t a2 = hist[(t + 2) * kMaxBins + b], a3 = hist[(t + 3) * kMaxBins + b];
+    offs[(t + 0) * kMaxBins + b] = run;
+    offs[(t + 1) * kMaxBins + b] = run + a0;
+    offs[(t + 2) * kMaxBins + b] = run + a0 + a1;
+    offs[(t + 3) * kMaxBins + b] = run + a0 + a1 + a2;
+    run += (uint64_t)a0 + a1 + a2 + a3;
+  }
+  for (; t < t1; t++) {
+    offs[t * kMaxBins + b] = run;
+    run += hist[t * kMaxBins + b];
   }
 }
 
 // ---------------------------------------------------------------------------
 // scatter: rank one tile by digit, stage in LDS, write coalesced runs
 // ---------------------------------------------------------------------------
+// Column 0 holds the key in its low bytes (SoA: the key column; AoS: the
+// record's first <=8-byte slice). One memory round trip loads column 0, the
+// first payload column and this tile's bucket offsets together; stores are
+// never waited for (LDS-only barriers between columns), so a workgroup's
+// writes drain while the next tile (2 workgroups per CU) loads.
 template <typename KT, typename U>
-__global__ __launch_bounds__(kScatterThreads) void scatter_kernel(
+__global__ __launch_bounds__(kScatterThreads, 4) void scatter_kernel(
     const SortDesc* __restrict__ desc, const SegPlan* __restrict__ plan,
     const int32_t* __restrict__ tile_seg, const uint64_t* __restrict__ offs) {
   constexpr int NT = kScatterThreads;
   constexpr int IT = kScatterItems;
   constexpr int NW = NT / 64;
+  static_assert(kMaxBins <= NT, "one thread per bin");
   __shared__ uint64_t sval[kTile];
-  __shared__ uint16_t sbin[kTile];
   __shared__ uint16_t wc[NW][kMaxBins];
   __shared__ uint32_t bin_start[kMaxBins];
   __shared__ int64_t gdst[kMaxBins];
   __shared__ uint32_t scan_sh[NW + 1];
 
-  const int64_t t = blockIdx.x;
+  const int64_t t = xcd_remap(blockIdx.x, gridDim.x);
   const int32_t s = tile_seg[t];
   const SegPlan P = plan[s];
   if (P.skip) return;
@@ -421,228 +623,490 @@ __global__ __launch_bounds__(kScatterThreads) void scatter_kernel(
   const uint32_t lane = lane_id();
   Xform<U> xf;
   xf.init(*desc);
-  const char* kp = desc->key.base[P.buf];
-  const uint32_t ks = desc->key.stride;
+  const int ncols = desc->ncols;
+  const int kbytes = desc->key_bits >> 3;
+  const uint64_t kmask = kbytes == 8 ? ~0ull : ((1ull << (8 * kbytes)) - 1);
+  // (columns are read field by field from the descriptor: a local copy of
+  // Col indexed by a run-time buffer id would live in scratch memory)
+  const uint32_t w0 = desc->cols[0].width, st0 = desc->cols[0].stride;
 
-  for (uint32_t i = threadIdx.x; i < (uint32_t)(NW * kMaxBins); i += NT)
-    (&wc[0][0])[i] = 0;
+  for (uint32_t i = threadIdx.x; i < (uint32_t)(NW * kMaxBins); i += NT) (&wc[0][0])[i] = 0;
 
   const int64_t base = P.start + tl * kTile;
   const int64_t rem = P.len - tl * kTile;
   const int cnt = rem < kTile ? (int)rem : kTile;
 
-  // striped tile layout: slot k of lane l of wave w = element w*IT*64 + k*64 + l
-  U raw[IT];
-  bool valid[IT];
-  uint32_t dig[IT];
+  // ---- one round trip: column 0 (key), column 1, bucket offsets ----------
+  const int ebase = (int)wave * IT * 64 + (int)lane;  // element of slot k: ebase + 64 k
+  uint64_t v0[IT], v1[IT];
+  {
+    const char* src = desc->cols[0].base[P.buf];
 #pragma unroll
-  for (int k = 0; k < IT; k++) {
-    const int e = (int)wave * IT * 64 + k * 64 + (int)lane;
-    valid[k] = e < cnt;
-    raw[k] = valid[k] ? (U) * (const KT*)(kp + (base + e) * (int64_t)ks) : (U)0;
+    for (int k = 0; k < IT; k++) {
+      const int e = ebase + k * 64;
+      v0[k] = e < cnt ? load_w(src + (base + e) * (int64_t)st0, w0) : 0;
+    }
   }
+  if (ncols > 1) {
+    const char* src = desc->cols[1].base[P.buf];
+    const uint32_t w1 = desc->cols[1].width, st1 = desc->cols[1].stride;
 #pragma unroll
-  for (int k = 0; k < IT; k++) dig[k] = (uint32_t)(xf(raw[k]) >> P.shift) & mask;
-  __syncthreads();  // wc zeroed
+    for (int k = 0; k < IT; k++) {
+      const int e = ebase + k * 64;
+      v1[k] = e < cnt ? load_w(src + (base + e) * (int64_t)st1, w1) : 0;
+    }
+  }
+  const uint32_t my_bin = threadIdx.x;
+  int64_t my_off = 0;
+  if (my_bin < nb) my_off = (int64_t)offs[t * kMaxBins + my_bin];
+
+  auto digit = [&](int k) -> uint32_t {
+    return (uint32_t)(xf((U)(v0[k] & kmask)) >> P.shift) & mask;
+  };
+  auto valid = [&](int k) -> bool { return ebase + k * 64 < cnt; };
+  lds_barrier();  // wc zeroed
 
   uint32_t pos[IT];
-  wlms_rank<IT>(dig, valid, P.bits, &wc[wave][0], pos);
-  __syncthreads();
+  wlms_rank_fn<IT>(digit, valid, P.bits, &wc[wave][0], pos);
+  lds_barrier();
 
-  // bin totals over waves -> per-wave exclusive offsets; tile exclusive scan
-  {
-    const uint32_t b0 = threadIdx.x * 2, b1 = b0 + 1;
-    uint32_t t0 = 0, t1 = 0;
-    if (b0 < nb) {
+  {  // per-bin totals over waves -> per-wave exclusive offsets; tile scan
+    uint32_t tb = 0;
+    if (my_bin < nb) {
 #pragma unroll
-      for (int w = 0; w < NW; w++) { const uint32_t c = wc[w][b0]; wc[w][b0] = (uint16_t)t0; t0 += c; }
-    }
-    if (b1 < nb) {
-#pragma unroll
-      for (int w = 0; w < NW; w++) { const uint32_t c = wc[w][b1]; wc[w][b1] = (uint16_t)t1; t1 += c; }
+      for (int w = 0; w < NW; w++) {
+        const uint32_t c = wc[w][my_bin];
+        wc[w][my_bin] = (uint16_t)tb;
+        tb += c;
+      }
     }
     uint32_t tot;
-    const uint32_t ex = block_excl_scan<NT>(t0 + t1, scan_sh, &tot);
-    if (b0 < nb) {
-      bin_start[b0] = ex;
-      const uint64_t o = offs[P.hist_base + (int64_t)b0 * P.ntiles + tl] - offs[P.hist_base];
-      gdst[b0] = P.start + (int64_t)o - (int64_t)ex;
-    }
-    if (b1 < nb) {
-      bin_start[b1] = ex + t0;
-      const uint64_t o = offs[P.hist_base + (int64_t)b1 * P.ntiles + tl] - offs[P.hist_base];
-      gdst[b1] = P.start + (int64_t)o - (int64_t)(ex + t0);
+    const uint32_t ex = block_excl_scan_lds<NT>(tb, scan_sh, &tot);
+    if (my_bin < nb) {
+      bin_start[my_bin] = ex;
+      gdst[my_bin] = P.start + my_off - (int64_t)ex;
     }
   }
-  __syncthreads();
+  lds_barrier();
 
 #pragma unroll
   for (int k = 0; k < IT; k++) {
-    if (valid[k]) {
-      const uint32_t d = dig[k];
+    if (valid(k)) {
+      const uint32_t d = digit(k);
       pos[k] = bin_start[d] + wc[wave][d] + pos[k];
-      sbin[pos[k]] = (uint16_t)d;
+      sval[pos[k]] = v0[k];
     }
   }
-  __syncthreads();
+  lds_barrier();
 
-  int64_t dst[IT];
-#pragma unroll
-  for (int i = 0; i < IT; i++) {
-    const int j = i * NT + (int)threadIdx.x;
-    dst[i] = j < cnt ? (int64_t)j + gdst[sbin[j]] : 0;
-  }
-
-  const int ncols = desc->ncols;
-  for (int c = 0; c < ncols; c++) {
-    const Col col = desc->cols[c];
-    const char* src = col.base[P.buf];
-    char* out = col.base[P.dst];
-    const uint32_t w = col.width, st = col.stride;
-    if (c == 0 && desc->col0_is_key) {
-#pragma unroll
-      for (int k = 0; k < IT; k++)
-        if (valid[k]) sval[pos[k]] = (uint64_t)raw[k];
-    } else {
-      uint64_t v[IT];
-#pragma unroll
-      for (int k = 0; k < IT; k++) {
-        const int e = (int)wave * IT * 64 + k * 64 + (int)lane;
-        v[k] = valid[k] ? load_w(src + (base + e) * (int64_t)st, w) : 0;
-      }
-#pragma unroll
-      for (int k = 0; k < IT; k++)
-        if (valid[k]) sval[pos[k]] = v[k];
-    }
-    __syncthreads();
+  // column 0: output slot j's bucket comes from the key itself
+  uint16_t dout[IT];
+  {
+    char* out = desc->cols[0].base[P.dst];
 #pragma unroll
     for (int i = 0; i < IT; i++) {
       const int j = i * NT + (int)threadIdx.x;
-      if (j < cnt) store_w(out + dst[i] * (int64_t)st, w, sval[j]);
+      dout[i] = 0;
+      if (j < cnt) {
+        const uint64_t x = sval[j];
+        const uint32_t d = (uint32_t)(xf((U)(x & kmask)) >> P.shift) & mask;
+        dout[i] = (uint16_t)d;
+        store_w(out + ((int64_t)j + gdst[d]) * (int64_t)st0, w0, x);
+      }
     }
-    __syncthreads();
+  }
+
+  for (int c = 1; c < ncols; c++) {
+    const uint32_t cw = desc->cols[c].width, cst = desc->cols[c].stride;
+    if (c > 1) {
+      const char* src = desc->cols[c].base[P.buf];
+#pragma unroll
+      for (int k = 0; k < IT; k++) {
+        const int e = ebase + k * 64;
+        v1[k] = e < cnt ? load_w(src + (base + e) * (int64_t)cst, cw) : 0;
+      }
+    }
+    lds_barrier();  // every slot of the previous column has been read
+#pragma unroll
+    for (int k = 0; k < IT; k++)
+      if (valid(k)) sval[pos[k]] = v1[k];
+    lds_barrier();
+    char* out = desc->cols[c].base[P.dst];
+#pragma unroll
+    for (int i = 0; i < IT; i++) {
+      const int j = i * NT + (int)threadIdx.x;
+      if (j < cnt) store_w(out + ((int64_t)j + gdst[dout[i]]) * (int64_t)cst, cw, sval[j]);
+    }
   }
 }
 
 // ---------------------------------------------------------------------------
-// local: one workgroup sorts one segment (<= kLocalCap keys) in LDS
+// local: one workgroup sorts one segment (<= CAP keys) in LDS
 // ---------------------------------------------------------------------------
-template <typename KT, typename U>
-__global__ __launch_bounds__(kLocalThreads) void local_kernel(
-    const SortDesc* __restrict__ desc, const Seg* __restrict__ segs) {
-  constexpr int NT = kLocalThreads;
+// Finishes the recursion for a segment that fits in LDS (the reference's
+// leaf, CmpSorterInsertionSort radixSort.hpp:159-178, plus every bit level
+// below it):
+//   1. keys and the first two columns are loaded once, coalesced;
+//   2. bucket pass on the top kLocalBits varying bits with LDS atomics
+//      (order inside a bucket is arbitrary here);
+//   3. if every bucket holds <= kRankSortMax keys: each key's final slot is
+//      bucket start + #(keys in its bucket ordered before it by
+//      (key, original index)) -> a stable order, computed in lockstep over
+//      the bucket so that LDS reads overlap;
+//      otherwise (skewed data): stable LSD digit passes (ballot ranks) over
+//      all varying bits;
+//   4. every column is staged in LDS in input order and written in output
+//      order: coalesced both ways, and safe in place.
+constexpr int kLocalBits = 9;
+constexpr int kRankSortMax = 96;
+
+// Stable ballot-ranked digit pass (fallback path): writes (u, id) in digit
+// order to su / sidx.
+template <int NT, int IT, typename U>
+__device__ __forceinline__ void local_digit_pass(
+    const U (&u)[IT], const uint32_t (&id)[IT], const bool (&valid)[IT], int sh, int nbits,
+    U* su, uint16_t* sidx, uint16_t (*wc)[1 << kLocalBits], uint32_t* bin_start,
+    uint32_t* scan_sh) {
+  constexpr int NW = NT / 64;
+  constexpr int BPT = (1 << kLocalBits) / NT;  // bins per thread
+  static_assert(BPT >= 1 && BPT * NT == (1 << kLocalBits), "bins per thread");
+  const uint32_t wave = threadIdx.x >> 6;
+  const uint32_t nb = 1u << nbits, mask = nb - 1;
+  for (uint32_t i = threadIdx.x; i < (uint32_t)(NW << kLocalBits); i += NT) (&wc[0][0])[i] = 0;
+  uint32_t dig[IT];
+#pragma unroll
+  for (int k = 0; k < IT; k++) dig[k] = (uint32_t)(u[k] >> sh) & mask;
+  lds_barrier();
+  uint32_t rank[IT];
+  wlms_rank<IT>(dig, valid, nbits, &wc[wave][0], rank);
+  lds_barrier();
+  {
+    uint32_t tb[BPT], tsum = 0;
+#pragma unroll
+    for (int q = 0; q < BPT; q++) {
+      const uint32_t b = threadIdx.x * BPT + q;
+      tb[q] = 0;
+      if (b < nb) {
+#pragma unroll
+        for (int w = 0; w < NW; w++) {
+          const uint32_t c = wc[w][b];
+          wc[w][b] = (uint16_t)tb[q];
+          tb[q] += c;
+        }
+      }
+      tsum += tb[q];
+    }
+    uint32_t tot;
+    uint32_t ex = block_excl_scan_lds<NT>(tsum, scan_sh, &tot);
+#pragma unroll
+    for (int q = 0; q < BPT; q++) {
+      const uint32_t b = threadIdx.x * BPT + q;
+      if (b < nb) bin_start[b] = ex;
+      ex += tb[q];
+    }
+  }
+  lds_barrier();
+#pragma unroll
+  for (int k = 0; k < IT; k++) {
+    if (valid[k]) {
+      const uint32_t p = bin_start[dig[k]] + wc[wave][dig[k]] + rank[k];
+      su[p] = u[k];
+      sidx[p] = (uint16_t)id[k];
+    }
+  }
+  lds_barrier();
+}
+
+template <typename KT, typename U, int NT>
+__global__ __launch_bounds__(NT) void local_kernel(const SortDesc* __restrict__ desc,
+                                                   const Seg* __restrict__ segs,
+                                                   Seg* __restrict__ fallback,
+                                                   unsigned long long* fallback_count) {
   constexpr int IT = kLocalItems;
   constexpr int NW = NT / 64;
-  constexpr int RB = 8;  // bits per LDS pass
-  __shared__ U su[kLocalCap];
-  __shared__ uint16_t sidx[kLocalCap];
-  __shared__ uint16_t wc[NW][1 << RB];
-  __shared__ uint32_t bin_start[1 << RB];
+  constexpr int CAP = NT * IT;
+  constexpr int NB = 1 << kLocalBits;
+  constexpr int BPT = NB / NT;
+  __shared__ uint64_t sbuf[CAP];          // keys (as U) during the sort, then column staging
+  __shared__ uint16_t sidx[CAP];          // bucket order -> original index
+  __shared__ uint16_t perm[CAP];          // output slot -> original index
+  __shared__ uint32_t hist[NB];           // bucket sizes, then insertion cursors
+  __shared__ uint32_t bin_start[NB + 1];
   __shared__ uint32_t scan_sh[NW + 1];
   __shared__ unsigned long long sh_or;
+  __shared__ int maxlen;
+  U* su = (U*)sbuf;
 
   const Seg g = segs[blockIdx.x];
   const uint32_t wave = threadIdx.x >> 6;
   const uint32_t lane = lane_id();
+  const int ebase = (int)wave * IT * 64 + (int)lane;  // element of slot k: ebase + 64 k
   Xform<U> xf;
   xf.init(*desc);
-  const char* kp = desc->key.base[g.buf];
-  const uint32_t ks = desc->key.stride;
   const int cnt = (int)g.len;
   const int64_t base = g.start;
-
-  if (threadIdx.x == 0) sh_or = 0;
-  U u[IT];
-  uint32_t id[IT];
-  bool valid[IT];
-#pragma unroll
-  for (int k = 0; k < IT; k++) {
-    const int e = (int)wave * IT * 64 + k * 64 + (int)lane;
-    valid[k] = e < cnt;
-    id[k] = (uint32_t)e;
-    u[k] = valid[k] ? (U) * (const KT*)(kp + (base + e) * (int64_t)ks) : (U)0;
-  }
-  const U uref = xf((U) * (const KT*)(kp + base * (int64_t)ks));
-  U vor = 0;
-#pragma unroll
-  for (int k = 0; k < IT; k++) {
-    u[k] = xf(u[k]);
-    if (valid[k]) vor |= u[k] ^ uref;
-  }
-  __syncthreads();
-  if (vor) atomicOr(&sh_or, (unsigned long long)vor);
-  __syncthreads();
-  const unsigned long long var = sh_or;
-
-  bool sorted_identity = (var == 0);
-  if (!sorted_identity) {
-    const int lo = __ffsll((long long)var) - 1;
-    const int hi = 63 - __clzll((long long)var);
-    for (int sh = lo; sh <= hi; sh += RB) {
-      const int nbits = (hi - sh + 1) < RB ? (hi - sh + 1) : RB;
-      const uint32_t nb = 1u << nbits, mask = nb - 1;
-      for (uint32_t i = threadIdx.x; i < (uint32_t)(NW << RB); i += NT) (&wc[0][0])[i] = 0;
-      uint32_t dig[IT];
-#pragma unroll
-      for (int k = 0; k < IT; k++) dig[k] = (uint32_t)(u[k] >> sh) & mask;
-      __syncthreads();
-      uint32_t rank[IT];
-      wlms_rank<IT>(dig, valid, nbits, &wc[wave][0], rank);
-      __syncthreads();
-      {
-        const uint32_t b = threadIdx.x;  // NT >= 256 bins
-        uint32_t tb = 0;
-        if (b < nb) {
-#pragma unroll
-          for (int w = 0; w < NW; w++) { const uint32_t c = wc[w][b]; wc[w][b] = (uint16_t)tb; tb += c; }
-        }
-        uint32_t tot;
-        const uint32_t ex = block_excl_scan<NT>(tb, scan_sh, &tot);
-        if (b < nb) bin_start[b] = ex;
-      }
-      __syncthreads();
-#pragma unroll
-      for (int k = 0; k < IT; k++) {
-        if (valid[k]) {
-          const uint32_t p = bin_start[dig[k]] + wc[wave][dig[k]] + rank[k];
-          su[p] = u[k];
-          sidx[p] = (uint16_t)id[k];
-        }
-      }
-      __syncthreads();
-#pragma unroll
-      for (int k = 0; k < IT; k++) {
-        const int e = (int)wave * IT * 64 + k * 64 + (int)lane;
-        if (valid[k]) {
-          u[k] = su[e];
-          id[k] = sidx[e];
-        }
-      }
-      __syncthreads();
-    }
-  }
-
-  // Move every column: out[start + e] = src[start + id(e)]. Register-staged
-  // with a barrier between all loads and all stores, so src == out (segment
-  // already in the output buffer) is safe.
-  if (sorted_identity && g.buf == BUF_OUT) return;
   const int ncols = desc->ncols;
-  for (int c = 0; c < ncols; c++) {
-    const Col col = desc->cols[c];
-    const char* src = col.base[g.buf];
-    char* out = col.base[BUF_OUT];
-    const uint32_t w = col.width, st = col.stride;
-    uint64_t v[IT];
-#pragma unroll
-    for (int k = 0; k < IT; k++)
-      v[k] = valid[k] ? load_w(src + (base + (int64_t)id[k]) * st, w) : 0;
-    __syncthreads();
+  const int kbytes = desc->key_bits >> 3;
+  const uint64_t kmask = kbytes == 8 ? ~0ull : ((1ull << (8 * kbytes)) - 1);
+
+  if (threadIdx.x == 0) {
+    sh_or = 0;
+    maxlen = 0;
+  }
+  for (uint32_t i = threadIdx.x; i < (uint32_t)NB; i += NT) hist[i] = 0;
+
+  // ---- 1. keys (column 0 holds the key in its low bytes) -------------------
+  uint64_t v0[IT];
+  {
+    const char* src = desc->cols[0].base[g.buf];
+    const uint32_t w = desc->cols[0].width, st = desc->cols[0].stride;
 #pragma unroll
     for (int k = 0; k < IT; k++) {
-      const int e = (int)wave * IT * 64 + k * 64 + (int)lane;
-      if (valid[k]) store_w(out + (base + e) * (int64_t)st, w, v[k]);
+      const int e = ebase + k * 64;
+      v0[k] = e < cnt ? load_w(src + (base + e) * (int64_t)st, w) : 0;
+    }
+  }
+  const U uref = xf((U)(load_w(desc->cols[0].base[g.buf] + base * (int64_t)desc->cols[0].stride,
+                               desc->cols[0].width) & kmask));
+  // keys and original indices are recomputed from v0 / the slot when needed
+  // (keeping them in registers costs occupancy)
+  auto ukey = [&](int k) -> U { return xf((U)(v0[k] & kmask)); };
+  auto valid = [&](int k) -> bool { return ebase + k * 64 < cnt; };
+  U vor = 0;
+#pragma unroll
+  for (int k = 0; k < IT; k++)
+    if (valid(k)) vor |= ukey(k) ^ uref;
+  if (vor) atomicOr(&sh_or, (unsigned long long)vor);
+  lds_barrier();
+  const unsigned long long var = sh_or;
+
+  if (var != 0) {
+    const int lo = __ffsll((long long)var) - 1;
+    const int hi = 63 - __clzll((long long)var);
+    const int nbits = (hi - lo + 1) < kLocalBits ? (hi - lo + 1) : kLocalBits;
+    const int sh = hi - nbits + 1;
+    const uint32_t mask = (1u << nbits) - 1;
+    // ---- 2. bucket pass (LDS atomics) ---------------------------------------
+#pragma unroll
+    for (int k = 0; k < IT; k++)
+      if (valid(k)) atomicAdd(&hist[(uint32_t)(ukey(k) >> sh) & mask], 1u);
+    lds_barrier();
+    {
+      uint32_t tb[BPT], tsum = 0;
+#pragma unroll
+      for (int q = 0; q < BPT; q++) {
+        tb[q] = hist[threadIdx.x * BPT + q];
+        tsum += tb[q];
+      }
+      uint32_t tot;
+      uint32_t ex = block_excl_scan_lds<NT>(tsum, scan_sh, &tot);
+      int mymax = 0;
+#pragma unroll
+      for (int q = 0; q < BPT; q++) {
+        bin_start[threadIdx.x * BPT + q] = ex;
+        hist[threadIdx.x * BPT + q] = ex;  // becomes the insertion cursor
+        ex += tb[q];
+        mymax = (int)tb[q] > mymax ? (int)tb[q] : mymax;
+      }
+      if (threadIdx.x == 0) bin_start[NB] = tot;
+      if (mymax > 0) atomicMax(&maxlen, mymax);
+    }
+    lds_barrier();
+    const int mlen = maxlen;
+    if (mlen <= kRankSortMax) {
+#pragma unroll
+      for (int k = 0; k < IT; k++) {
+        if (valid(k)) {
+          const U uk = ukey(k);
+          const uint32_t p = atomicAdd(&hist[(uint32_t)(uk >> sh) & mask], 1u);
+          su[p] = uk;
+          sidx[p] = (uint16_t)(ebase + k * 64);
+        }
+      }
+      lds_barrier();
+      // ---- 3. rank inside each bucket by (key, original index) -------------
+      // (slots in two halves to bound register use; results go straight to
+      // perm, a different array than the one being read)
+      constexpr int H = IT / 2;
+#pragma unroll
+      for (int half = 0; half < 2; half++) {
+        U x[H];
+        uint32_t bs[H], bl[H], xid[H], r[H];
+        int wmax = 0;
+#pragma unroll
+        for (int i = 0; i < H; i++) {
+          const int p = (half * H + i) * NT + (int)threadIdx.x;
+          bl[i] = 0;
+          bs[i] = 0;
+          x[i] = 0;
+          xid[i] = 0;
+          r[i] = 0;
+          if (p < cnt) {
+            x[i] = su[p];
+            xid[i] = sidx[p];
+            const uint32_t d = (uint32_t)(x[i] >> sh) & mask;
+            bs[i] = bin_start[d];
+            bl[i] = bin_start[d + 1] - bs[i];
+            wmax = (int)bl[i] > wmax ? (int)bl[i] : wmax;
+          }
+        }
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) {
+          const int t2 = __shfl_xor(wmax, o, 64);
+          wmax = t2 > wmax ? t2 : wmax;
+        }
+        for (int j = 0; j < wmax; j++) {
+#pragma unroll
+          for (int i = 0; i < H; i++) {
+            if ((uint32_t)j < bl[i]) {
+              const U y = su[bs[i] + j];
+              const uint32_t yid = sidx[bs[i] + j];
+              r[i] += (y < x[i]) | ((y == x[i]) & (yid < xid[i]));
+            }
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < H; i++) {
+          const int p = (half * H + i) * NT + (int)threadIdx.x;
+          if (p < cnt) perm[r[i] + bs[i]] = (uint16_t)xid[i];
+        }
+      }
+      lds_barrier();
+    } else {
+      // skewed bucket sizes: hand the segment to local_lsd_kernel (nothing
+      // has been written to global memory yet)
+      if (threadIdx.x == 0) fallback[atomicAdd(fallback_count, 1ull)] = g;
+      return;
+    }
+  } else if (g.buf == BUF_OUT) {
+    return;  // all keys equal and already home
+  } else {
+#pragma unroll
+    for (int k = 0; k < IT; k++) perm[ebase + k * 64] = (uint16_t)(ebase + k * 64);
+    lds_barrier();
+  }
+  // output slot e takes input element perm[e]
+  uint32_t id[IT];
+#pragma unroll
+  for (int k = 0; k < IT; k++) id[k] = perm[ebase + k * 64];
+
+  // ---- 4. columns: stage in input order, write in output order --------------
+  // (column 0 is re-read from L2 rather than held in registers through the
+  // sort; in place is safe: every load of a column completes before the
+  // barrier that precedes its stores)
+  for (int c = 0; c < ncols; c++) {
+    const char* src = desc->cols[c].base[g.buf];
+    char* out = desc->cols[c].base[BUF_OUT];
+    const uint32_t w = desc->cols[c].width, st = desc->cols[c].stride;
+    uint64_t v[IT];
+#pragma unroll
+    for (int k = 0; k < IT; k++) {
+      const int e = ebase + k * 64;
+      v[k] = e < cnt ? load_w(src + (base + e) * (int64_t)st, w) : 0;
+    }
+    lds_barrier();  // previous users of sbuf are done
+#pragma unroll
+    for (int k = 0; k < IT; k++)
+      if (valid(k)) sbuf[ebase + k * 64] = v[k];
+    lds_barrier();
+#pragma unroll
+    for (int k = 0; k < IT; k++) {
+      const int e = ebase + k * 64;
+      if (valid(k)) store_w(out + (base + e) * (int64_t)st, w, sbuf[id[k]]);
+    }
+  }
+}
+
+// Fallback for segments whose top-digit buckets are too large for the rank
+// step (skewed keys): stable LSD passes (ballot ranks) over every varying
+// bit. Grid-stride over a device-side list whose length is read on device.
+template <typename KT, typename U>
+__global__ __launch_bounds__(kLocalThreads) void local_lsd_kernel(
+    const SortDesc* __restrict__ desc, const Seg* __restrict__ segs,
+    const unsigned long long* __restrict__ nsegs) {
+  constexpr int NT = kLocalThreads;
+  constexpr int IT = kLocalItems;
+  constexpr int NW = NT / 64;
+  constexpr int CAP = NT * IT;
+  constexpr int NB = 1 << kLocalBits;
+  __shared__ uint64_t sbuf[CAP];
+  __shared__ uint16_t sidx[CAP];
+  __shared__ uint16_t wc[NW][NB];
+  __shared__ uint32_t bin_start[NB + 1];
+  __shared__ uint32_t scan_sh[NW + 1];
+  __shared__ unsigned long long sh_or;
+  U* su = (U*)sbuf;
+  const uint32_t wave = threadIdx.x >> 6;
+  const int ebase = (int)wave * IT * 64 + (int)lane_id();
+  Xform<U> xf;
+  xf.init(*desc);
+  const int ncols = desc->ncols;
+  const int kbytes = desc->key_bits >> 3;
+  const uint64_t kmask = kbytes == 8 ? ~0ull : ((1ull << (8 * kbytes)) - 1);
+  const unsigned long long total = *nsegs;
+  for (unsigned long long si = blockIdx.x; si < total; si += gridDim.x) {
+    const Seg g = segs[si];
+    const int cnt = (int)g.len;
+    const int64_t base = g.start;
+    __syncthreads();
+    if (threadIdx.x == 0) sh_or = 0;
+    U u[IT];
+    uint32_t id[IT];
+    bool valid[IT];
+    {
+      const char* src = desc->cols[0].base[g.buf];
+      const uint32_t w = desc->cols[0].width, st = desc->cols[0].stride;
+#pragma unroll
+      for (int k = 0; k < IT; k++) {
+        const int e = ebase + k * 64;
+        valid[k] = e < cnt;
+        id[k] = (uint32_t)e;
+        u[k] = valid[k] ? xf((U)(load_w(src + (base + e) * (int64_t)st, w) & kmask)) : (U)0;
+      }
     }
     __syncthreads();
+    const U uref = xf((U)(load_w(desc->cols[0].base[g.buf] + base * (int64_t)desc->cols[0].stride,
+                                 desc->cols[0].width) & kmask));
+    U vor = 0;
+#pragma unroll
+    for (int k = 0; k < IT; k++)
+      if (valid[k]) vor |= u[k] ^ uref;
+    if (vor) atomicOr(&sh_or, (unsigned long long)vor);
+    __syncthreads();
+    const unsigned long long var = sh_or;
+    if (var != 0) {
+      const int lo = __ffsll((long long)var) - 1;
+      const int hi = 63 - __clzll((long long)var);
+      for (int s0 = lo; s0 <= hi; s0 += kLocalBits) {
+        const int nb2 = (hi - s0 + 1) < kLocalBits ? (hi - s0 + 1) : kLocalBits;
+        local_digit_pass<NT, IT, U>(u, id, valid, s0, nb2, su, sidx, wc, bin_start, scan_sh);
+#pragma unroll
+        for (int k = 0; k < IT; k++) {
+          const int e = ebase + k * 64;
+          if (valid[k]) {
+            u[k] = su[e];
+            id[k] = sidx[e];
+          }
+        }
+        __syncthreads();
+      }
+    }
+    // register gather, barrier between all loads and all stores (in place safe)
+    for (int c = 0; c < ncols; c++) {
+      const char* src = desc->cols[c].base[g.buf];
+      char* out = desc->cols[c].base[BUF_OUT];
+      const uint32_t w = desc->cols[c].width, st = desc->cols[c].stride;
+      uint64_t v[IT];
+#pragma unroll
+      for (int k = 0; k < IT; k++)
+        v[k] = valid[k] ? load_w(src + (base + (int64_t)id[k]) * st, w) : 0;
+      __syncthreads();
+#pragma unroll
+      for (int k = 0; k < IT; k++) {
+        const int e = ebase + k * 64;
+        if (valid[k]) store_w(out + (base + e) * (int64_t)st, w, v[k]);
+      }
+    }
   }
 }
 
@@ -698,26 +1162,26 @@ __global__ void fill_kernel(int64_t n, int kind, uint64_t seed, uint64_t first,
   }
 
 void launch_plan(const Seg* big, int64_t nbig, SegPlan* plan, int64_t* tcount,
-                 int64_t* hcount, unsigned long long* var_or, uint64_t* elems,
+                 int64_t* gcount, unsigned long long* var_or, uint64_t* elems,
                  hipStream_t st) {
   plan_kernel<<<(unsigned)((nbig + 255) / 256), 256, 0, st>>>(big, nbig, plan, tcount,
-                                                              hcount, var_or, elems);
+                                                              gcount, var_or, elems);
 }
 
 void launch_plan_bases(SegPlan* plan, int64_t nbig, const int64_t* tbase,
-                       const int64_t* hbase, hipStream_t st) {
+                       const int64_t* gbase, hipStream_t st) {
   plan_bases_kernel<<<(unsigned)((nbig + 255) / 256), 256, 0, st>>>(plan, nbig, tbase,
-                                                                    hbase);
+                                                                    gbase);
 }
 
-void launch_tile_map(const SegPlan* plan, int64_t nbig, int64_t ntiles, int32_t* tile_seg,
-                     hipStream_t st) {
-  tile_map_kernel<<<(unsigned)((ntiles + 255) / 256), 256, 0, st>>>(plan, nbig, ntiles,
-                                                                    tile_seg);
+void launch_seg_map(const int64_t* bases, int64_t nbig, int64_t n, int32_t* out,
+                    hipStream_t st) {
+  if (n > 0)
+    seg_map_kernel<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(bases, nbig, n, out);
 }
 
 void launch_count(int key_size, const SortDesc* d, const SegPlan* plan,
-                  const int32_t* tile_seg, int64_t ntiles, uint64_t* hist,
+                  const int32_t* tile_seg, int64_t ntiles, uint32_t* hist,
                   unsigned long long* var_or, hipStream_t st) {
 #define CALL(KT, U)                                                                  \
   count_kernel<KT, U><<<(unsigned)ntiles, kScatterThreads, 0, st>>>(d, plan, tile_seg, \
@@ -736,11 +1200,15 @@ void launch_excl_scan(const uint64_t* x, uint64_t* y, int64_t n, uint64_t* temp,
   if (nb > 0) scan_apply_kernel<<<(unsigned)nb, kScanThreads, 0, st>>>(x, n, temp, y);
 }
 
-void launch_children(SegPlan* plan, int64_t nbig, const uint64_t* offs,
-                     const unsigned long long* var_or, Seg* big_next, Seg* local,
-                     Seg* copy, ListCounters* ctr, hipStream_t st) {
-  children_kernel<<<(unsigned)nbig, 512, 0, st>>>(plan, offs, var_or, big_next, local,
-                                                  copy, ctr);
+void launch_offsets(SegPlan* plan, int64_t nbig, const int32_t* group_seg, int64_t ngroups,
+                    const uint32_t* hist, uint32_t* gsum, uint64_t* gofs, uint64_t* sbase,
+                    uint64_t* offs, const unsigned long long* var_or, Seg* big_next,
+                    Seg* local, Seg* local2, Seg* copy, ListCounters* ctr, hipStream_t st) {
+  group_sum_kernel<<<(unsigned)ngroups, kMaxBins, 0, st>>>(plan, group_seg, hist, gsum);
+  seg_scan_kernel<<<(unsigned)nbig, kMaxBins, 0, st>>>(plan, gsum, gofs, sbase, var_or,
+                                                      big_next, local, local2, copy, ctr);
+  tile_offs_kernel<<<(unsigned)ngroups, kMaxBins, 0, st>>>(plan, group_seg, hist, gofs, sbase,
+                                                          offs);
 }
 
 void launch_scatter(int key_size, const SortDesc* d, const SegPlan* plan,
@@ -752,9 +1220,22 @@ void launch_scatter(int key_size, const SortDesc* d, const SegPlan* plan,
 #undef CALL
 }
 
-void launch_local(int key_size, const SortDesc* d, const Seg* segs, int64_t nsegs,
-                  hipStream_t st) {
-#define CALL(KT, U) local_kernel<KT, U><<<(unsigned)nsegs, kLocalThreads, 0, st>>>(d, segs)
+void launch_local(int key_size, const SortDesc* d, const Seg* segs, int64_t nsegs, int big_class,
+                  Seg* fallback, unsigned long long* fallback_count, hipStream_t st) {
+#define CALL(KT, U)                                                                  \
+  if (big_class)                                                                     \
+    local_kernel<KT, U, kLocalThreads>                                               \
+        <<<(unsigned)nsegs, kLocalThreads, 0, st>>>(d, segs, fallback, fallback_count); \
+  else                                                                               \
+    local_kernel<KT, U, kLocalThreadsSmall>                                          \
+        <<<(unsigned)nsegs, kLocalThreadsSmall, 0, st>>>(d, segs, fallback, fallback_count)
+  SRS_KEY_DISPATCH(key_size, CALL)
+#undef CALL
+}
+
+void launch_local_lsd(int key_size, const SortDesc* d, const Seg* segs,
+                      const unsigned long long* nsegs, int grid, hipStream_t st) {
+#define CALL(KT, U) local_lsd_kernel<KT, U><<<(unsigned)grid, kLocalThreads, 0, st>>>(d, segs, nsegs)
   SRS_KEY_DISPATCH(key_size, CALL)
 #undef CALL
 }
@@ -776,13 +1257,16 @@ __global__ void set_desc_kernel(SortDesc d, SortDesc* out) {
 }
 
 __global__ void init_lists_kernel(Seg seg0, int to_local, Seg* big, Seg* local,
-                                  ListCounters* ctr) {
+                                  Seg* local2, ListCounters* ctr) {
   if (threadIdx.x == 0) {
     ctr->n_big = to_local ? 0 : 1;
-    ctr->n_local = to_local ? 1 : 0;
+    const bool small = seg0.len <= kLocalCapSmall;
+    ctr->n_local = (to_local && small) ? 1 : 0;
+    ctr->n_local2 = (to_local && !small) ? 1 : 0;
     ctr->n_copy = 0;
+    ctr->n_fallback = 0;
     ctr->local_elems = to_local ? (unsigned long long)seg0.len : 0;
-    if (to_local) local[0] = seg0; else big[0] = seg0;
+    if (to_local) (small ? local : local2)[0] = seg0; else big[0] = seg0;
   }
 }
 
@@ -790,9 +1274,9 @@ void launch_set_desc(const SortDesc& d, SortDesc* out, hipStream_t st) {
   set_desc_kernel<<<1, 64, 0, st>>>(d, out);
 }
 
-void launch_init_lists(Seg seg0, int to_local, Seg* big, Seg* local, ListCounters* ctr,
-                       hipStream_t st) {
-  init_lists_kernel<<<1, 64, 0, st>>>(seg0, to_local, big, local, ctr);
+void launch_init_lists(Seg seg0, int to_local, Seg* big, Seg* local, Seg* local2,
+                       ListCounters* ctr, hipStream_t st) {
+  init_lists_kernel<<<1, 64, 0, st>>>(seg0, to_local, big, local, local2, ctr);
 }
 
 }  // namespace srs

@@ -1,0 +1,43 @@
+"""The reference's correctness matrix (src/test.cpp) re-expressed in C++
+against the drop-in header include/simd_sort/radix_sort.hpp (tests/cpp/
+test_dropin.cpp): {Separate, Combined} x {Up, Down} x 10 key types x 14
+payload packs x 8 distributions x n in {1, 10, 100, 1000, 10000}."""
+import os
+import subprocess
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CPP = os.path.join(REPO, "tests", "cpp")
+BIN = os.path.join(CPP, "_build", "test_dropin")
+
+
+def test_dropin_header_compiles_without_avx512():
+    """The drop-in header needs no AVX-512 (unlike the reference's)."""
+    src = ('#include "simd_sort/radix_sort.hpp"\n'
+           "int main(){ unsigned long long k[4]={3,1,2,0}; float p[4]={0,1,2,3};\n"
+           " simd_sort::radix_sort::sort(4, k, p);\n"
+           " simd_sort::DataElement<unsigned, unsigned> e[2]{};\n"
+           " simd_sort::radix_sort::sort<false>(2, e);\n"
+           " return 0; }\n")
+    subprocess.run(["g++", "-std=c++17", "-mno-avx512f", "-fsyntax-only", "-x", "c++",
+                    "-I", os.path.join(REPO, "include"), "-"], input=src.encode(), check=True)
+
+
+def test_dropin_rejects_non_power_of_two_element_at_compile_time():
+    src = ('#include "simd_sort/radix_sort.hpp"\n'
+           "int main(){ simd_sort::DataElement<float, unsigned, unsigned> e[2]{};\n"
+           " simd_sort::radix_sort::sort(2, e); return 0; }\n")
+    r = subprocess.run(["g++", "-std=c++17", "-fsyntax-only", "-x", "c++",
+                        "-I", os.path.join(REPO, "include"), "-"], input=src.encode(),
+                       capture_output=True)
+    assert r.returncode != 0 and b"power of two" in r.stderr
+
+
+@pytest.mark.gpu
+def test_dropin_matrix_on_gpu():
+    if not os.path.exists(BIN):
+        subprocess.run(["make", "-C", CPP], check=True)
+    r = subprocess.run([BIN, "10000", "42"], capture_output=True, text=True, timeout=900)
+    tail = "\n".join(r.stdout.splitlines()[-12:])
+    assert r.returncode == 0 and "All tests passed" in r.stdout, tail + r.stderr[-2000:]
