@@ -36,6 +36,8 @@ CONFIGS = {
     "c1": ("u64", [8], "soa", "1e9 uint64 keys + one uint64 payload column, uniform random"),
     "c2": ("f32", [4, 4], "soa", "1e9 float32 keys + two uint32 payload columns"),
     "c3": ("u64", [8], "aos", "1e9 DataElement<uint64,uint64> combined AoS array"),
+    "k64": ("u64", [], "soa", "uint64 keys only (diagnostic)"),
+    "k32": ("u32", [], "soa", "uint32 keys only (C0 shape)"),
 }
 
 
@@ -54,7 +56,7 @@ def parse():
 
 def kind_id(name):
     import srs_amd
-    return {"u64": srs_amd.KEY_U64, "f32": srs_amd.KEY_F32}[name]
+    return {"u64": srs_amd.KEY_U64, "f32": srs_amd.KEY_F32, "u32": srs_amd.KEY_U32}[name]
 
 
 # ---------------------------------------------------------------------------
@@ -66,7 +68,7 @@ def cpu_baseline(cfg_name, n_sample):
     from srs_testlib import (KIND_DTYPES, oracle_sort_aos, oracle_sort_soa, ref_lib,
                              ref_sort_aos, ref_sort_soa)
     kname, psizes, layout, _ = CONFIGS[cfg_name]
-    kind = {"u64": 6, "f32": 8}[kname]
+    kind = {"u64": 6, "f32": 8, "u32": 4}[kname]
     n = int(n_sample)
     # same generator as the device fill (srs_fill_synthetic_device)
     idx = np.arange(n, dtype=np.uint64) + np.uint64(42 << 32)
@@ -138,7 +140,7 @@ def main():
     n = int(args.n)
 
     tdt = {8: torch.int64, 4: torch.int32}
-    key_dt = torch.int64 if kname == "u64" else torch.float32
+    key_dt = {"u64": torch.int64, "f32": torch.float32, "u32": torch.int32}[kname]
     keys = torch.empty(n, dtype=key_dt, device=dev)
     pays = [torch.empty(n, dtype=tdt[s], device=dev) for s in psizes]
     srs_amd.fill_synthetic_device(keys, *pays, seed=42 << 32, first_index=rank * n, key_kind=kind)
@@ -156,12 +158,16 @@ def main():
     torch.cuda.synchronize()
 
     if world > 1:
-        from srs_dist import ShardSorter  # noqa: E402  (multi-GPU path)
-        sorter = ShardSorter(kind, n, psizes, dev)
+        if layout != "soa":
+            raise SystemExit("multi-GPU bench runs the SoA configs (c1, c2)")
+        from srs_amd.dist import HipShardOps, ShardSorter  # multi-GPU path (RCCL)
+        sorter = ShardSorter(HipShardOps(kind), n, [p.dtype for p in pays], keys.dtype, dev)
+    shard_out = []
 
     def step():
         if world > 1:
-            return sorter.sort(keys, pays)
+            shard_out[:] = [sorter.sort(keys, pays)]
+            return
         if layout == "aos":
             srs_amd.sort_combined_device(rec, kind, out=rec_out)
         else:
@@ -224,6 +230,8 @@ def main():
     if not args.no_verify and world == 1:
         verified = verify(keys_out if layout == "soa" else None, pays_out if layout == "soa" else None,
                           rec_out, kname, torch)
+    elif not args.no_verify:
+        verified = verify_shards(keys, pays, shard_out[0], kname, torch, dist, dev)
 
     cpu = None
     if rank == 0 and args.cpu_sample > 0 and (world == 1):
@@ -263,6 +271,48 @@ def main():
         dist.destroy_process_group()
 
 
+def _order_view(k, kname, torch):
+    if kname == "u64":
+        return k ^ torch.iinfo(torch.int64).min  # unsigned order as signed
+    if kname == "u32":
+        return k.to(torch.int64) & 0xFFFFFFFF
+    return k
+
+
+def _hash_pairs(k, p, torch):
+    """Order-independent checksum of (key, payload) pairs: sum of a mixed
+    64-bit hash (wrapping int64 arithmetic)."""
+    kk = k.view(torch.int64) if k.element_size() == 8 else k.view(torch.int32).to(torch.int64)
+    pp = p.view(torch.int64) if p.element_size() == 8 else p.view(torch.int32).to(torch.int64)
+    x = kk * 0x9E3779B97F4A7C15 + pp
+    x = x ^ ((x >> 29) & 0x7FFFFFFFF)
+    x = x * 0xBF58476D1CE4E5B9
+    return int(x.sum().item())
+
+
+def verify_shards(keys_in, pays_in, out, kname, torch, dist, dev):
+    """Multi-GPU: each rank sorted; last key of rank r <= first of rank r+1;
+    the multiset of (key, payload) pairs over all ranks is unchanged."""
+    k, ps = out
+    s = _order_view(k, kname, torch)
+    ok = bool((s[1:] >= s[:-1]).all().item()) if s.numel() > 1 else True
+    ends = torch.tensor([float(s[0].item()) if s.numel() else float("inf"),
+                         float(s[-1].item()) if s.numel() else float("-inf")],
+                        dtype=torch.float64, device=dev)
+    world = dist.get_world_size()
+    allends = [torch.zeros_like(ends) for _ in range(world)]
+    dist.all_gather(allends, ends)
+    nonempty = [e.tolist() for e in allends if e[0].item() != float("inf")]
+    bounds_ok = all(a[1] <= b[0] for a, b in zip(nonempty, nonempty[1:]))
+    h = torch.tensor([_hash_pairs(keys_in, pays_in[0], torch), _hash_pairs(k, ps[0], torch),
+                      keys_in.numel(), k.numel()], dtype=torch.int64, device=dev)
+    dist.all_reduce(h)
+    okt = torch.tensor([1 if ok else 0], device=dev)
+    dist.all_reduce(okt, op=dist.ReduceOp.MIN)
+    return {"sorted": bool(okt.item()), "rank_bounds_ordered": bounds_ok,
+            "multiset_hash_equal": h[0].item() == h[1].item(), "count_equal": h[2].item() == h[3].item()}
+
+
 def verify(keys_out, pays_out, rec_out, kname, torch):
     """Size-independent checks on the full output: sortedness (transformed
     order) and payload == f(key) for every element; plus count preserved."""
@@ -271,11 +321,8 @@ def verify(keys_out, pays_out, rec_out, kname, torch):
         p = [rec_out[:, 1]]
     else:
         k, p = keys_out, pays_out
-    if kname == "u64":
-        s = (k ^ torch.iinfo(torch.int64).min)  # unsigned order as signed
-        ok = bool((s[1:] >= s[:-1]).all().item())
-    else:
-        ok = bool((k[1:] >= k[:-1]).all().item())
+    s = _order_view(k, kname, torch)
+    ok = bool((s[1:] >= s[:-1]).all().item())
     return {"sorted": ok}
 
 

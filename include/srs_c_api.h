@@ -112,11 +112,41 @@ int srs_sort_aos_device(int64_t num, int key_kind, int up,
                         int64_t cmp_sort_threshold, void* elements,
                         uint32_t elem_size, void* elements_out, void* stream);
 
+/* ---- multi-GPU shard primitives (top-radix-bits partition) --
+ * A node-wide sort of one array spread over N GPUs: every rank histograms
+ * its keys' top bits (srs_key_histogram_device), the histograms are summed
+ * (RCCL all-reduce), contiguous bucket ranges are assigned to ranks, every
+ * rank partitions its keys by destination (srs_partition_device), the groups
+ * are exchanged (RCCL all-to-all) and each rank sorts what it received
+ * (srs_sort_soa_device). Concatenating the ranks in order gives the sorted
+ * array. The reference has no multi-device path; these have no counterpart. */
+
+/* Adds the histogram of the transformed top `bits` (1..12) bits of `num`
+ * device keys into the device array hist[2^bits] (uint64). Asynchronous. */
+int srs_key_histogram_device(int64_t num, int key_kind, int up, const void* keys,
+                             int bits, uint64_t* hist, void* stream);
+
+/* Stable partition of a key column and its payload columns into num_parts
+ * (<= 512) groups: a key whose transformed top `bits` (1..16) bits equal b
+ * goes to group part_of_bucket[b] (DEVICE int32 array of 2^bits entries;
+ * non-decreasing makes every group a contiguous key range). Groups are
+ * written back to back, group 0 first, to keys_out / payloads_out (device,
+ * not aliasing the inputs); part_counts (HOST array of num_parts int64)
+ * receives the group sizes. Returns after the counts are known; the data
+ * movement completes on `stream`. */
+int srs_partition_device(int64_t num, int key_kind, int up, const void* keys,
+                         int32_t num_payloads, const void* const* payloads,
+                         const uint32_t* payload_sizes, int bits,
+                         const int32_t* part_of_bucket, int32_t num_parts,
+                         void* keys_out, void* const* payloads_out,
+                         int64_t* part_counts, void* stream);
+
 /* ---- synthetic data (bench / tests) ------------------------------------- */
 
 /* keys[i] = splitmix64(seed + first_index + i) truncated/reinterpreted to the
  * key kind (floats: uniform in [-1,1) on a 2^-23 / 2^-52 grid); payload column
- * c gets bytes of splitmix64(bits(key[i]) + c) (a function of the key). */
+ * c gets the low bytes of splitmix64(bits(key[i]) ^ c * 0xD1B54A32D192ED03)
+ * (a function of the key). */
 int srs_fill_synthetic_device(int64_t num, int key_kind, uint64_t seed,
                               uint64_t first_index, void* keys,
                               int32_t num_payloads, void* const* payloads,
@@ -139,6 +169,11 @@ int srs_set_kernel_timing(int enable);
 int srs_reset_kernel_stats(void);
 int srs_kernel_stats(const char* name, int64_t* launches, double* total_ms,
                      double* elements);
+
+/* Diagnostic builds only (-DSRS_STAMPS=1): device buffer of 64 uint64 that
+ * accumulates per-phase s_memtime cycles of the scatter (slots 0..15) and
+ * local (16..31) kernels; NULL disables. No effect in the product build. */
+int srs_debug_set_stamp_buffer(void* device_acc);
 
 /* Release cached device workspaces (for leak checks / shutdown). */
 int srs_release_workspace(void);

@@ -30,6 +30,7 @@ namespace srs {
 namespace {
 
 thread_local std::string g_err = "no error";
+unsigned long long* g_stamp_acc = nullptr;  // srs_debug_set_stamp_buffer
 
 int fail(int code, const std::string& msg) {
   g_err = msg;
@@ -245,6 +246,94 @@ void key_masks(int kind, int up, SortDesc& d) {
   d.key_bits = kb;
 }
 
+struct LevelState {
+  int64_t nbig, n_local, n_local2, n_copy;
+  int cur;
+};
+
+// One global MSB level over every large segment in W->big[S.cur]:
+// plan -> bases -> count -> offsets + children -> scatter. Children go to
+// W->big[S.cur ^ 1] / the local lists / the copy list; S is updated from the
+// device counters. force_bits / lut: partition passes (srs_partition_device).
+int run_level(Workspace* W, int ks, const SortDesc* d_desc, LevelState& S, int force_bits,
+              bool lut, hipStream_t st) {
+  const int64_t nbig = S.nbig;
+  ListCounters* d_ctr = (ListCounters*)W->ctr.p;
+  uint64_t* d_totals = (uint64_t*)W->totals.p;
+  // ---- plan + tile / scan-group bases
+  SRS_TRY(ensure(W->plan, nbig * sizeof(SegPlan)));
+  SRS_TRY(ensure(W->tcount, nbig * 8));
+  SRS_TRY(ensure(W->gcount, nbig * 8));
+  SRS_TRY(ensure(W->tbase, nbig * 8));
+  SRS_TRY(ensure(W->gbase, nbig * 8));
+  SRS_TRY(ensure(W->var, nbig * 8));
+  SRS_TRY(ensure(W->sbase, (size_t)nbig * kMaxBins * 8));
+  SRS_TRY(ensure(W->scan_tmp, scan_temp_elems(nbig) * 8));
+  SegPlan* plan = (SegPlan*)W->plan.p;
+  unsigned long long* var = (unsigned long long*)W->var.p;
+  {
+    TimedScope ts("plan", (double)nbig, st);
+    HIP_TRY(hipMemsetAsync(d_totals + 3, 0, sizeof(uint64_t), st));
+    launch_plan((Seg*)W->big[S.cur].p, nbig, plan, (int64_t*)W->tcount.p,
+                (int64_t*)W->gcount.p, var, d_totals + 3, force_bits, st);
+    launch_excl_scan((uint64_t*)W->tcount.p, (uint64_t*)W->tbase.p, nbig,
+                     (uint64_t*)W->scan_tmp.p, d_totals + 0, st);
+    launch_excl_scan((uint64_t*)W->gcount.p, (uint64_t*)W->gbase.p, nbig,
+                     (uint64_t*)W->scan_tmp.p, d_totals + 1, st);
+    launch_plan_bases(plan, nbig, (int64_t*)W->tbase.p, (int64_t*)W->gbase.p, st);
+  }
+  HIP_TRY(hipMemcpyAsync(W->h_totals, d_totals, 4 * sizeof(uint64_t),
+                         hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  const int64_t ntiles = (int64_t)W->h_totals[0];
+  const int64_t ngroups = (int64_t)W->h_totals[1];
+  const double level_elems = (double)W->h_totals[3];
+  note_elems("count", level_elems);
+  note_elems("scatter", level_elems);
+
+  SRS_TRY(ensure(W->tile_seg, ntiles * 4));
+  SRS_TRY(ensure(W->group_seg, ngroups * 4));
+  SRS_TRY(ensure(W->hist, (size_t)ntiles * kMaxBins * 4));
+  SRS_TRY(ensure(W->offs, (size_t)ntiles * kMaxBins * 8));
+  SRS_TRY(ensure(W->gsum, (size_t)ngroups * kMaxBins * 4));
+  SRS_TRY(ensure(W->gofs, (size_t)ngroups * kMaxBins * 8));
+  int32_t* tile_seg = (int32_t*)W->tile_seg.p;
+  int32_t* group_seg = (int32_t*)W->group_seg.p;
+  launch_seg_map((int64_t*)W->tbase.p, nbig, ntiles, tile_seg, st);
+  launch_seg_map((int64_t*)W->gbase.p, nbig, ngroups, group_seg, st);
+  {
+    TimedScope ts("count", (double)0, st);
+    launch_count(ks, d_desc, plan, tile_seg, ntiles, (uint32_t*)W->hist.p, var, lut, st);
+  }
+  // ---- offsets + children (list capacity for the worst case: every bin non-empty)
+  const size_t worst = (size_t)nbig * kMaxBins;
+  const int nxt = S.cur ^ 1;
+  SRS_TRY(ensure(W->big[nxt], worst * sizeof(Seg)));
+  SRS_TRY(ensure_keep(W->local, (S.n_local + worst) * sizeof(Seg), S.n_local * sizeof(Seg), st));
+  SRS_TRY(ensure_keep(W->local2, (S.n_local2 + worst) * sizeof(Seg), S.n_local2 * sizeof(Seg), st));
+  SRS_TRY(ensure_keep(W->copy, (S.n_copy + worst) * sizeof(Seg), S.n_copy * sizeof(Seg), st));
+  HIP_TRY(hipMemsetAsync(&d_ctr->n_big, 0, sizeof(unsigned long long), st));
+  {
+    TimedScope ts("scan", (double)ntiles, st);
+    launch_offsets(plan, nbig, group_seg, ngroups, (uint32_t*)W->hist.p,
+                   (uint32_t*)W->gsum.p, (uint64_t*)W->gofs.p, (uint64_t*)W->sbase.p,
+                   (uint64_t*)W->offs.p, var, (Seg*)W->big[nxt].p, (Seg*)W->local.p,
+                   (Seg*)W->local2.p, (Seg*)W->copy.p, d_ctr, st);
+  }
+  {
+    TimedScope ts("scatter", (double)0, st);
+    launch_scatter(ks, d_desc, plan, tile_seg, (uint64_t*)W->offs.p, ntiles, lut, st);
+  }
+  HIP_TRY(hipMemcpyAsync(W->h_ctr, d_ctr, sizeof(ListCounters), hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  S.nbig = (int64_t)W->h_ctr->n_big;
+  S.n_local = (int64_t)W->h_ctr->n_local;
+  S.n_local2 = (int64_t)W->h_ctr->n_local2;
+  S.n_copy = (int64_t)W->h_ctr->n_copy;
+  S.cur = nxt;
+  return SRS_OK;
+}
+
 int run_sort(Workspace* W, const Request& R, hipStream_t st) {
   const int ks = key_size_of(R.kind);
   const int64_t n = R.num;
@@ -294,6 +383,7 @@ int run_sort(Workspace* W, const Request& R, hipStream_t st) {
   if (inplace)  // IN aliases OUT: a segment that never moved is already home
     for (int c = 0; c < d.ncols; c++) d.cols[c].base[BUF_IN] = d.cols[c].base[BUF_OUT];
 
+  d.stamp_acc = g_stamp_acc;
   SRS_TRY(ensure(W->desc, sizeof(SortDesc)));
   SortDesc* d_desc = (SortDesc*)W->desc.p;
   launch_set_desc(d, d_desc, st);
@@ -314,87 +404,19 @@ int run_sort(Workspace* W, const Request& R, hipStream_t st) {
   launch_init_lists(seg0, to_local ? 1 : 0, (Seg*)W->big[0].p, (Seg*)W->local.p,
                     (Seg*)W->local2.p, d_ctr, st);
 
-  int64_t nbig = to_local ? 0 : 1;
   int64_t n_local = (to_local && n <= kLocalCapSmall) ? 1 : 0;
   int64_t n_local2 = (to_local && n > kLocalCapSmall) ? 1 : 0;
   int64_t n_copy = 0;
   W->h_ctr->local_elems = to_local ? (uint64_t)n : 0;
-  int cur = 0;
+  LevelState S{to_local ? 0 : 1, n_local, n_local2, n_copy, 0};
   int level = 0;
-  while (nbig > 0) {
+  while (S.nbig > 0) {
     if (++level > 80) return fail(SRS_ERR_INTERNAL, "level limit exceeded");
-    // ---- plan + tile / scan-group bases
-    SRS_TRY(ensure(W->plan, nbig * sizeof(SegPlan)));
-    SRS_TRY(ensure(W->tcount, nbig * 8));
-    SRS_TRY(ensure(W->gcount, nbig * 8));
-    SRS_TRY(ensure(W->tbase, nbig * 8));
-    SRS_TRY(ensure(W->gbase, nbig * 8));
-    SRS_TRY(ensure(W->var, nbig * 8));
-    SRS_TRY(ensure(W->sbase, (size_t)nbig * kMaxBins * 8));
-    SRS_TRY(ensure(W->scan_tmp, scan_temp_elems(nbig) * 8));
-    SegPlan* plan = (SegPlan*)W->plan.p;
-    unsigned long long* var = (unsigned long long*)W->var.p;
-    {
-      TimedScope ts("plan", (double)nbig, st);
-      HIP_TRY(hipMemsetAsync(d_totals + 3, 0, sizeof(uint64_t), st));
-      launch_plan((Seg*)W->big[cur].p, nbig, plan, (int64_t*)W->tcount.p,
-                  (int64_t*)W->gcount.p, var, d_totals + 3, st);
-      launch_excl_scan((uint64_t*)W->tcount.p, (uint64_t*)W->tbase.p, nbig,
-                       (uint64_t*)W->scan_tmp.p, d_totals + 0, st);
-      launch_excl_scan((uint64_t*)W->gcount.p, (uint64_t*)W->gbase.p, nbig,
-                       (uint64_t*)W->scan_tmp.p, d_totals + 1, st);
-      launch_plan_bases(plan, nbig, (int64_t*)W->tbase.p, (int64_t*)W->gbase.p, st);
-    }
-    HIP_TRY(hipMemcpyAsync(W->h_totals, d_totals, 4 * sizeof(uint64_t),
-                           hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipStreamSynchronize(st));
-    const int64_t ntiles = (int64_t)W->h_totals[0];
-    const int64_t ngroups = (int64_t)W->h_totals[1];
-    const double level_elems = (double)W->h_totals[3];
-    note_elems("count", level_elems);
-    note_elems("scatter", level_elems);
-
-    SRS_TRY(ensure(W->tile_seg, ntiles * 4));
-    SRS_TRY(ensure(W->group_seg, ngroups * 4));
-    SRS_TRY(ensure(W->hist, (size_t)ntiles * kMaxBins * 4));
-    SRS_TRY(ensure(W->offs, (size_t)ntiles * kMaxBins * 8));
-    SRS_TRY(ensure(W->gsum, (size_t)ngroups * kMaxBins * 4));
-    SRS_TRY(ensure(W->gofs, (size_t)ngroups * kMaxBins * 8));
-    int32_t* tile_seg = (int32_t*)W->tile_seg.p;
-    int32_t* group_seg = (int32_t*)W->group_seg.p;
-    launch_seg_map((int64_t*)W->tbase.p, nbig, ntiles, tile_seg, st);
-    launch_seg_map((int64_t*)W->gbase.p, nbig, ngroups, group_seg, st);
-    {
-      TimedScope ts("count", (double)0, st);
-      launch_count(ks, d_desc, plan, tile_seg, ntiles, (uint32_t*)W->hist.p, var, st);
-    }
-    // ---- offsets + children (list capacity for the worst case: every bin non-empty)
-    const size_t worst = (size_t)nbig * kMaxBins;
-    const int nxt = cur ^ 1;
-    SRS_TRY(ensure(W->big[nxt], worst * sizeof(Seg)));
-    SRS_TRY(ensure_keep(W->local, (n_local + worst) * sizeof(Seg), n_local * sizeof(Seg), st));
-    SRS_TRY(ensure_keep(W->local2, (n_local2 + worst) * sizeof(Seg), n_local2 * sizeof(Seg), st));
-    SRS_TRY(ensure_keep(W->copy, (n_copy + worst) * sizeof(Seg), n_copy * sizeof(Seg), st));
-    HIP_TRY(hipMemsetAsync(&d_ctr->n_big, 0, sizeof(unsigned long long), st));
-    {
-      TimedScope ts("scan", (double)ntiles, st);
-      launch_offsets(plan, nbig, group_seg, ngroups, (uint32_t*)W->hist.p,
-                     (uint32_t*)W->gsum.p, (uint64_t*)W->gofs.p, (uint64_t*)W->sbase.p,
-                     (uint64_t*)W->offs.p, var, (Seg*)W->big[nxt].p, (Seg*)W->local.p,
-                     (Seg*)W->local2.p, (Seg*)W->copy.p, d_ctr, st);
-    }
-    {
-      TimedScope ts("scatter", (double)0, st);
-      launch_scatter(ks, d_desc, plan, tile_seg, (uint64_t*)W->offs.p, ntiles, st);
-    }
-    HIP_TRY(hipMemcpyAsync(W->h_ctr, d_ctr, sizeof(ListCounters), hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipStreamSynchronize(st));
-    nbig = (int64_t)W->h_ctr->n_big;
-    n_local = (int64_t)W->h_ctr->n_local;
-    n_local2 = (int64_t)W->h_ctr->n_local2;
-    n_copy = (int64_t)W->h_ctr->n_copy;
-    cur = nxt;
+    SRS_TRY(run_level(W, ks, d_desc, S, 0, false, st));
   }
+  n_local = S.n_local;
+  n_local2 = S.n_local2;
+  n_copy = S.n_copy;
 
   if (n_local + n_local2 > 0) {
     note_elems("local", (double)W->h_ctr->local_elems);
@@ -429,6 +451,60 @@ int run_sort(Workspace* W, const Request& R, hipStream_t st) {
     }
   }
   HIP_TRY(hipGetLastError());
+  return SRS_OK;
+}
+
+// One LUT-digit level: stable partition of the columns into num_parts groups
+// (multi-GPU shard). The scatter's destination buffer (TMP) is
+// the caller's output arrays.
+int run_partition(Workspace* W, const Request& R, int bits, const int32_t* d_lut,
+                  int nparts, int64_t* counts, hipStream_t st) {
+  const int ks = key_size_of(R.kind);
+  const int64_t n = R.num;
+  SortDesc d;
+  memset(&d, 0, sizeof d);
+  key_masks(R.kind, R.up, d);
+  for (int c = 0; c < R.ncols; c++) {
+    char* in = (char*)R.in_cols[c];
+    char* out = (char*)R.out_cols[c];
+    d.cols[c] = Col{{in, out, out}, R.widths[c], R.widths[c]};
+  }
+  d.key = d.cols[0];
+  d.ncols = R.ncols;
+  d.digit_lut = d_lut;
+  d.lut_shift = d.key_bits - bits;
+  SRS_TRY(ensure(W->desc, sizeof(SortDesc)));
+  SortDesc* d_desc = (SortDesc*)W->desc.p;
+  launch_set_desc(d, d_desc, st);
+  SRS_TRY(ensure(W->big[0], 1024 * sizeof(Seg)));
+  SRS_TRY(ensure(W->big[1], 1024 * sizeof(Seg)));
+  SRS_TRY(ensure(W->local, 1024 * sizeof(Seg)));
+  SRS_TRY(ensure(W->local2, 1024 * sizeof(Seg)));
+  SRS_TRY(ensure(W->copy, 1024 * sizeof(Seg)));
+  SRS_TRY(ensure(W->ctr, sizeof(ListCounters)));
+  SRS_TRY(ensure(W->totals, 4 * sizeof(uint64_t)));
+  Seg seg0{0, n, d.key_bits, BUF_IN};
+  launch_init_lists(seg0, 0, (Seg*)W->big[0].p, (Seg*)W->local.p, (Seg*)W->local2.p,
+                    (ListCounters*)W->ctr.p, st);
+  int fb = 1;
+  while ((1 << fb) < nparts) fb++;
+  LevelState S{1, 0, 0, 0, 0};
+  SRS_TRY(run_level(W, ks, d_desc, S, fb, true, st));
+  // group sizes from the segment's bucket bases (sbase row 0)
+  std::vector<uint64_t> sb((size_t)1 << fb);
+  HIP_TRY(hipMemcpyAsync(sb.data(), W->sbase.p, sb.size() * 8, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  bool single = false;
+  for (int p = 0; p < nparts; p++) {
+    const uint64_t lo = sb[p], hi = (p + 1 < (int)sb.size()) ? sb[p + 1] : (uint64_t)n;
+    counts[p] = p + 1 < nparts ? (int64_t)(hi - lo) : (int64_t)((uint64_t)n - lo);
+    single |= counts[p] == n;
+  }
+  if (single) {  // the scatter was skipped (one group holds everything): copy
+    for (int c = 0; c < R.ncols; c++)
+      HIP_TRY(hipMemcpyAsync(R.out_cols[c], R.in_cols[c], (size_t)n * R.widths[c],
+                             hipMemcpyDeviceToDevice, st));
+  }
   return SRS_OK;
 }
 
@@ -616,6 +692,60 @@ int srs_fill_synthetic_device(int64_t num, int key_kind, uint64_t seed, uint64_t
   return SRS_OK;
 }
 
+int srs_key_histogram_device(int64_t num, int key_kind, int up, const void* keys, int bits,
+                             uint64_t* hist, void* stream) {
+  const int ks = key_size_of(key_kind);
+  if (ks == 0) return fail(SRS_ERR_INVALID_ARG, "invalid key_kind");
+  if (bits < 1 || bits > kHistMaxBits || bits > 8 * ks)
+    return fail(SRS_ERR_INVALID_ARG, "bits must be in [1, min(12, key bits)]");
+  if (num <= 0) return SRS_OK;
+  if (!keys || !hist) return fail(SRS_ERR_INVALID_ARG, "NULL pointer");
+  SortDesc d;
+  memset(&d, 0, sizeof d);
+  key_masks(key_kind, up, d);
+  launch_key_hist(ks, num, keys, d, bits, (unsigned long long*)hist, (hipStream_t)stream);
+  HIP_TRY(hipGetLastError());
+  return SRS_OK;
+}
+
+int srs_partition_device(int64_t num, int key_kind, int up, const void* keys,
+                         int32_t num_payloads, const void* const* payloads,
+                         const uint32_t* payload_sizes, int bits, const int32_t* part_of_bucket,
+                         int32_t num_parts, void* keys_out, void* const* payloads_out,
+                         int64_t* part_counts, void* stream) {
+  const int ks = key_size_of(key_kind);
+  if (ks == 0) return fail(SRS_ERR_INVALID_ARG, "invalid key_kind");
+  if (bits < 1 || bits > 16 || bits > 8 * ks)
+    return fail(SRS_ERR_INVALID_ARG, "bits must be in [1, min(16, key bits)]");
+  if (num_parts < 1 || num_parts > kMaxBins)
+    return fail(SRS_ERR_INVALID_ARG, "num_parts must be in [1, 512]");
+  if (!part_counts || !part_of_bucket) return fail(SRS_ERR_INVALID_ARG, "NULL pointer");
+  for (int p = 0; p < num_parts; p++) part_counts[p] = 0;
+  if (num <= 0) return SRS_OK;
+  Request R;
+  SRS_TRY(build_soa(R, num, key_kind, up, 0, (void*)keys, num_payloads, (void* const*)payloads,
+                    payload_sizes, keys_out, payloads_out));
+  if (!keys_out) return fail(SRS_ERR_INVALID_ARG, "keys_out is NULL");
+  if (num == 1) {
+    // a single key: its group from the table, then a plain copy
+    int32_t one = 0;
+    SortDesc d;
+    memset(&d, 0, sizeof d);
+    key_masks(key_kind, up, d);
+    uint64_t bitsv = 0;
+    HIP_TRY(hipMemcpy(&bitsv, keys, ks, hipMemcpyDeviceToHost));
+    uint64_t u = bitsv ^ ((bitsv & d.signbit) ? d.mneg : d.mpos);
+    HIP_TRY(hipMemcpy(&one, part_of_bucket + (u >> (8 * ks - bits)), 4, hipMemcpyDeviceToHost));
+    if (one < 0 || one >= num_parts) return fail(SRS_ERR_INVALID_ARG, "part id out of range");
+    part_counts[one] = 1;
+    return copy_through(R, (hipStream_t)stream);
+  }
+  std::lock_guard<std::mutex> lk(g_wmu);
+  Workspace* W = nullptr;
+  SRS_TRY(get_ws(&W));
+  return run_partition(W, R, bits, part_of_bucket, num_parts, part_counts, (hipStream_t)stream);
+}
+
 const char* srs_last_error(void) { return g_err.c_str(); }
 
 const char* srs_version(void) { return "srs_amd 0.1.0 gfx950"; }
@@ -642,6 +772,11 @@ int srs_kernel_stats(const char* name, int64_t* launches, double* total_ms, doub
   if (launches) *launches = k.launches;
   if (total_ms) *total_ms = k.ms;
   if (elements) *elements = k.elems;
+  return SRS_OK;
+}
+
+int srs_debug_set_stamp_buffer(void* device_acc) {
+  g_stamp_acc = (unsigned long long*)device_acc;
   return SRS_OK;
 }
 

@@ -40,6 +40,10 @@ struct SortDesc {
   int32_t canon_zero;      // float keys, n <= cmpSortThreshold: -0.0 == +0.0
   // transformed key u = bits ^ (bits & signbit ? mneg : mpos)
   uint64_t mpos, mneg, signbit, negzero;
+  // partition passes only: digit = digit_lut[u >> lut_shift]
+  const int32_t* digit_lut;
+  int32_t lut_shift;
+  unsigned long long* stamp_acc;  // diagnostic builds only (SRS_STAMPS)
 };
 
 struct Seg {
@@ -75,12 +79,32 @@ struct ListCounters {
 };
 
 // Tuning constants (see DESIGN.md §4 for how they were chosen).
-constexpr int kScatterThreads = 512;
-constexpr int kScatterItems = 12;
-constexpr int kTile = kScatterThreads * kScatterItems;   // 6144 keys per tile
+// (overridable at build time for tuning sweeps: tools/build_variants.sh)
+#ifndef SRS_SCATTER_THREADS
+#define SRS_SCATTER_THREADS 512
+#endif
+#ifndef SRS_SCATTER_ITEMS
+#define SRS_SCATTER_ITEMS 8
+#endif
+#ifndef SRS_SCATTER_WAVES_PER_EU
+#define SRS_SCATTER_WAVES_PER_EU 4
+#endif
+#ifndef SRS_SCATTER_PIPE
+#define SRS_SCATTER_PIPE 0
+#endif
+#ifndef SRS_SCATTER_WG_PER_CU
+#define SRS_SCATTER_WG_PER_CU 2
+#endif
+#ifndef SRS_LOCAL_KEEP_KEYS
+#define SRS_LOCAL_KEEP_KEYS 1
+#endif
+constexpr int kScatterThreads = SRS_SCATTER_THREADS;
+constexpr int kScatterItems = SRS_SCATTER_ITEMS;
+constexpr int kTile = kScatterThreads * kScatterItems;   // keys per tile
 constexpr int kMaxDigitBits = 9;
 constexpr int kMaxBins = 1 << kMaxDigitBits;   // histogram row stride (tile-major)
 constexpr int kScanGroup = 256;                 // tiles per column-scan group
+constexpr int kHistMaxBits = 12;                // srs_key_histogram_device
 
 constexpr int kLocalItems = 16;
 constexpr int kLocalThreads = 512;

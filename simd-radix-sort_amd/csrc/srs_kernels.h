@@ -9,7 +9,7 @@
 namespace srs {
 
 void launch_plan(const Seg* big, int64_t nbig, SegPlan* plan, int64_t* tcount,
-                 int64_t* gcount, unsigned long long* var_or, uint64_t* elems,
+                 int64_t* gcount, unsigned long long* var_or, uint64_t* elems, int force_bits,
                  hipStream_t st);
 void launch_plan_bases(SegPlan* plan, int64_t nbig, const int64_t* tbase,
                        const int64_t* gbase, hipStream_t st);
@@ -17,7 +17,7 @@ void launch_seg_map(const int64_t* bases, int64_t nbig, int64_t n, int32_t* out,
                     hipStream_t st);
 void launch_count(int key_size, const SortDesc* d, const SegPlan* plan,
                   const int32_t* tile_seg, int64_t ntiles, uint32_t* hist,
-                  unsigned long long* var_or, hipStream_t st);
+                  unsigned long long* var_or, bool lut, hipStream_t st);
 int64_t scan_temp_elems(int64_t n);
 void launch_excl_scan(const uint64_t* x, uint64_t* y, int64_t n, uint64_t* temp,
                       uint64_t* total, hipStream_t st);
@@ -26,8 +26,10 @@ void launch_offsets(SegPlan* plan, int64_t nbig, const int32_t* group_seg, int64
                     uint64_t* offs, const unsigned long long* var_or, Seg* big_next,
                     Seg* local, Seg* local2, Seg* copy, ListCounters* ctr, hipStream_t st);
 void launch_scatter(int key_size, const SortDesc* d, const SegPlan* plan,
-                    const int32_t* tile_seg, const uint64_t* offs, int64_t ntiles,
+                    const int32_t* tile_seg, const uint64_t* offs, int64_t ntiles, bool lut,
                     hipStream_t st);
+void launch_key_hist(int key_size, int64_t n, const void* keys, const SortDesc& d, int bits,
+                     unsigned long long* hist, hipStream_t st);
 void launch_local(int key_size, const SortDesc* d, const Seg* segs, int64_t nsegs, int big_class,
                   Seg* fallback, unsigned long long* fallback_count, hipStream_t st);
 void launch_local_lsd(int key_size, const SortDesc* d, const Seg* segs,

@@ -18,6 +18,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "srs_common.h"
 #include "srs_kernels.h"
 
@@ -65,6 +67,16 @@ struct Xform {
 
 __device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63; }
 
+// Digit of a transformed key for a global pass: the key's bits
+// [shift, shift + bits), or (LUT) a group id looked up by its top bits (the
+// multi-GPU partition, whose groups are contiguous ranges of top-bit buckets).
+template <bool LUT, typename U>
+__device__ __forceinline__ uint32_t pass_digit(U u, int shift, uint32_t mask, const int32_t* lut,
+                                               int lut_shift) {
+  if constexpr (LUT) return (uint32_t)lut[(uint64_t)u >> lut_shift];
+  else return (uint32_t)(u >> shift) & mask;
+}
+
 __device__ __forceinline__ uint32_t popc_below(uint64_t m) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
                                    __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
@@ -108,6 +120,36 @@ __device__ __forceinline__ T block_excl_scan(T v, T* sh, T* total) {
   return r;
 }
 
+// ---- diagnostic phase stamps (build with -DSRS_STAMPS=1; never in the product
+// build). Wave 0 drains its memory counters and reads s_memtime at each phase
+// boundary; per-phase cycles are summed over workgroups into
+// desc->stamp_acc[kernel * 16 + phase] (slot 0 counts workgroups).
+#ifndef SRS_STAMPS
+#define SRS_STAMPS 0
+#endif
+#if SRS_STAMPS
+#define STAMP_DECL unsigned long long ts_[8] = {0}; int tsn_ = 0;
+#define STAMP()                                                              \
+  do {                                                                       \
+    if (threadIdx.x == 0) {                                                  \
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");            \
+      if (tsn_ < 8) ts_[tsn_++] = __builtin_amdgcn_s_memtime();              \
+    }                                                                        \
+  } while (0)
+#define STAMP_FLUSH(kid)                                                     \
+  do {                                                                       \
+    if (threadIdx.x == 0 && desc->stamp_acc) {                               \
+      atomicAdd(&desc->stamp_acc[(kid) * 16], 1ull);                         \
+      for (int i_ = 1; i_ < tsn_; i_++)                                      \
+        atomicAdd(&desc->stamp_acc[(kid) * 16 + i_], ts_[i_] - ts_[i_ - 1]); \
+    }                                                                        \
+  } while (0)
+#else
+#define STAMP_DECL
+#define STAMP() do {} while (0)
+#define STAMP_FLUSH(kid) do {} while (0)
+#endif
+
 // Workgroup barrier that orders LDS accesses only. __syncthreads() also waits
 // for every outstanding global load AND store of the wave (s_waitcnt
 // vmcnt(0)); kernels that keep stores or prefetch loads in flight across a
@@ -146,7 +188,7 @@ __device__ __forceinline__ T block_excl_scan_lds(T v, T* sh, T* total) {
 // `wc`) plus the number of lower-lane peers. Items are in striped order
 // (slot k of lane l = wave-local element k * 64 + l), so ranks follow input
 // order within a digit.
-template <int ITEMS, typename DigitFn, typename ValidFn>
+template <int ITEMS, int MAXB = kMaxDigitBits, typename DigitFn, typename ValidFn>
 __device__ __forceinline__ void wlms_rank_fn(DigitFn digit, ValidFn valid, int nbits,
                                              uint16_t* wc, uint32_t (&rank)[ITEMS]) {
   const uint64_t lt = (lane_id() == 0) ? 0ull : (~0ull >> (64 - lane_id()));
@@ -156,7 +198,7 @@ __device__ __forceinline__ void wlms_rank_fn(DigitFn digit, ValidFn valid, int n
     uint64_t peers = __ballot(ok);
     const uint32_t d = digit(k);
 #pragma unroll
-    for (int b = 0; b < kMaxDigitBits; b++) {
+    for (int b = 0; b < MAXB; b++) {
       if (b < nbits) {
         const bool bit = (d >> b) & 1u;
         const uint64_t m = __ballot(bit);
@@ -231,7 +273,7 @@ __global__ void plan_kernel(const Seg* __restrict__ big, int64_t nbig,
                             SegPlan* __restrict__ plan, int64_t* __restrict__ tcount,
                             int64_t* __restrict__ gcount,
                             unsigned long long* __restrict__ var_or,
-                            uint64_t* __restrict__ elems) {
+                            uint64_t* __restrict__ elems, int force_bits) {
   const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= nbig) return;
   const Seg g = big[s];
@@ -239,8 +281,8 @@ __global__ void plan_kernel(const Seg* __restrict__ big, int64_t nbig,
   SegPlan p;
   p.start = g.start;
   p.len = g.len;
-  p.bits = choose_bits(g.len, g.rbits);
-  p.shift = g.rbits - p.bits;
+  p.bits = force_bits ? force_bits : choose_bits(g.len, g.rbits);
+  p.shift = force_bits ? 0 : g.rbits - p.bits;
   p.ntiles = (int32_t)((g.len + kTile - 1) / kTile);
   p.ngroups = (p.ntiles + kScanGroup - 1) / kScanGroup;
   p.buf = g.buf;
@@ -290,7 +332,7 @@ __device__ __forceinline__ int64_t xcd_remap(int64_t bid, int64_t nwg) {
 // ---------------------------------------------------------------------------
 // count: per-tile digit histogram (bin-major per segment) + varying bits
 // ---------------------------------------------------------------------------
-template <typename KT, typename U>
+template <typename KT, typename U, bool LUT>
 __global__ __launch_bounds__(kScatterThreads) void count_kernel(
     const SortDesc* __restrict__ desc, const SegPlan* __restrict__ plan,
     const int32_t* __restrict__ tile_seg, uint32_t* __restrict__ hist,
@@ -307,6 +349,8 @@ __global__ __launch_bounds__(kScatterThreads) void count_kernel(
   xf.init(*desc);
   const char* kp = desc->key.base[P.buf];
   const uint32_t ks = desc->key.stride;
+  const int32_t* lut = desc->digit_lut;
+  const int lut_shift = desc->lut_shift;
 
   for (uint32_t i = threadIdx.x; i < nb; i += kScatterThreads) h[i] = 0;
   if (threadIdx.x == 0) sh_or = 0;
@@ -328,7 +372,7 @@ __global__ __launch_bounds__(kScatterThreads) void count_kernel(
     const int e = k * kScatterThreads + threadIdx.x;
     if (e < cnt) {
       const U u = xf(raw[k]);
-      atomicAdd(&h[(uint32_t)(u >> P.shift) & mask], 1u);
+      atomicAdd(&h[pass_digit<LUT>(u, P.shift, mask, lut, lut_shift)], 1u);
       vor |= u ^ uref;
     }
   }
@@ -594,128 +638,153 @@ __global__ __launch_bounds__(kMaxBins) void tile_offs_kernel(
 // scatter: rank one tile by digit, stage in LDS, write coalesced runs
 // ---------------------------------------------------------------------------
 // Column 0 holds the key in its low bytes (SoA: the key column; AoS: the
-// record's first <=8-byte slice). One memory round trip loads column 0, the
-// first payload column and this tile's bucket offsets together; stores are
-// never waited for (LDS-only barriers between columns), so a workgroup's
-// writes drain while the next tile (2 workgroups per CU) loads.
+// record's first <=8-byte slice). A tile's loads (column 0, the first payload
+// column, its row of bucket offsets) are issued together; stores are never
+// waited for (LDS-only barriers between columns).
+//
+// scatter_pipe_kernel is persistent: each workgroup walks a contiguous chunk
+// of tiles and issues tile t+1's loads BEFORE tile t's ranking and stores
+// (vmcnt counts loads and stores in issue order, so a load issued after a
+// store would wait for it). HBM then always has a tile's worth of loads in
+// flight per workgroup, and neighbouring tiles' runs into one bucket are
+// written by one workgroup (their partial lines meet in one L2).
+struct ScatterLds {
+  uint64_t sval[kTile];
+  uint16_t wc[kScatterThreads / 64][kMaxBins];
+  uint32_t bin_start[kMaxBins];
+  int64_t gdst[kMaxBins];
+  uint32_t scan_sh[kScatterThreads / 64 + 1];
+};
+
+struct TileInfo {
+  int64_t base;   // first element of the tile
+  int32_t cnt;    // elements in the tile (0: skip)
+  int32_t s;      // segment
+};
+
 template <typename KT, typename U>
-__global__ __launch_bounds__(kScatterThreads, 4) void scatter_kernel(
+__device__ __forceinline__ TileInfo scatter_load_tile(
     const SortDesc* __restrict__ desc, const SegPlan* __restrict__ plan,
-    const int32_t* __restrict__ tile_seg, const uint64_t* __restrict__ offs) {
-  constexpr int NT = kScatterThreads;
+    const int32_t* __restrict__ tile_seg, const uint64_t* __restrict__ offs, int64_t t,
+    int ncols, uint64_t (&v0)[kScatterItems], uint64_t (&v1)[kScatterItems], int64_t& my_off) {
   constexpr int IT = kScatterItems;
-  constexpr int NW = NT / 64;
-  static_assert(kMaxBins <= NT, "one thread per bin");
-  __shared__ uint64_t sval[kTile];
-  __shared__ uint16_t wc[NW][kMaxBins];
-  __shared__ uint32_t bin_start[kMaxBins];
-  __shared__ int64_t gdst[kMaxBins];
-  __shared__ uint32_t scan_sh[NW + 1];
-
-  const int64_t t = xcd_remap(blockIdx.x, gridDim.x);
-  const int32_t s = tile_seg[t];
-  const SegPlan P = plan[s];
-  if (P.skip) return;
+  TileInfo ti;
+  ti.s = tile_seg[t];
+  const SegPlan P = plan[ti.s];
   const int64_t tl = t - P.tile_base;
-  const uint32_t nb = 1u << P.bits;
-  const uint32_t mask = nb - 1;
-  const uint32_t wave = threadIdx.x >> 6;
-  const uint32_t lane = lane_id();
-  Xform<U> xf;
-  xf.init(*desc);
-  const int ncols = desc->ncols;
-  const int kbytes = desc->key_bits >> 3;
-  const uint64_t kmask = kbytes == 8 ? ~0ull : ((1ull << (8 * kbytes)) - 1);
-  // (columns are read field by field from the descriptor: a local copy of
-  // Col indexed by a run-time buffer id would live in scratch memory)
-  const uint32_t w0 = desc->cols[0].width, st0 = desc->cols[0].stride;
-
-  for (uint32_t i = threadIdx.x; i < (uint32_t)(NW * kMaxBins); i += NT) (&wc[0][0])[i] = 0;
-
-  const int64_t base = P.start + tl * kTile;
+  ti.base = P.start + tl * kTile;
   const int64_t rem = P.len - tl * kTile;
-  const int cnt = rem < kTile ? (int)rem : kTile;
-
-  // ---- one round trip: column 0 (key), column 1, bucket offsets ----------
-  const int ebase = (int)wave * IT * 64 + (int)lane;  // element of slot k: ebase + 64 k
-  uint64_t v0[IT], v1[IT];
+  ti.cnt = P.skip ? 0 : (rem < kTile ? (int)rem : kTile);
+  const int ebase = (int)(threadIdx.x >> 6) * IT * 64 + (int)lane_id();
   {
     const char* src = desc->cols[0].base[P.buf];
+    const uint32_t w = desc->cols[0].width, st = desc->cols[0].stride;
 #pragma unroll
     for (int k = 0; k < IT; k++) {
       const int e = ebase + k * 64;
-      v0[k] = e < cnt ? load_w(src + (base + e) * (int64_t)st0, w0) : 0;
+      v0[k] = e < ti.cnt ? load_w(src + (ti.base + e) * (int64_t)st, w) : 0;
     }
   }
   if (ncols > 1) {
     const char* src = desc->cols[1].base[P.buf];
-    const uint32_t w1 = desc->cols[1].width, st1 = desc->cols[1].stride;
+    const uint32_t w = desc->cols[1].width, st = desc->cols[1].stride;
 #pragma unroll
     for (int k = 0; k < IT; k++) {
       const int e = ebase + k * 64;
-      v1[k] = e < cnt ? load_w(src + (base + e) * (int64_t)st1, w1) : 0;
+      v1[k] = e < ti.cnt ? load_w(src + (ti.base + e) * (int64_t)st, w) : 0;
     }
   }
-  const uint32_t my_bin = threadIdx.x;
-  int64_t my_off = 0;
-  if (my_bin < nb) my_off = (int64_t)offs[t * kMaxBins + my_bin];
+  my_off = 0;
+  if (ti.cnt > 0 && threadIdx.x < (1u << P.bits)) my_off = (int64_t)offs[t * kMaxBins + threadIdx.x];
+  return ti;
+}
 
+template <typename KT, typename U, bool LUT>
+__device__ __forceinline__ void scatter_process_tile(
+    const SortDesc* __restrict__ desc, const SegPlan* __restrict__ plan, ScatterLds& L,
+    const TileInfo& ti, int ncols, const uint64_t (&v0)[kScatterItems],
+    uint64_t (&v1)[kScatterItems], int64_t my_off) {
+  constexpr int NT = kScatterThreads;
+  constexpr int IT = kScatterItems;
+  constexpr int NW = NT / 64;
+  const SegPlan P = plan[ti.s];
+  const uint32_t nb = 1u << P.bits;
+  const uint32_t mask = nb - 1;
+  const uint32_t wave = threadIdx.x >> 6;
+  const int ebase = (int)wave * IT * 64 + (int)lane_id();
+  const int cnt = ti.cnt;
+  Xform<U> xf;
+  xf.init(*desc);
+  const int kbytes = desc->key_bits >> 3;
+  const uint64_t kmask = kbytes == 8 ? ~0ull : ((1ull << (8 * kbytes)) - 1);
+  const int32_t* lut = desc->digit_lut;
+  const int lut_shift = desc->lut_shift;
+  STAMP_DECL
+  STAMP();
+
+  lds_barrier();  // the previous tile's readers of L are done
+  for (uint32_t i = threadIdx.x; i < (uint32_t)(NW * kMaxBins); i += NT) (&L.wc[0][0])[i] = 0;
   auto digit = [&](int k) -> uint32_t {
-    return (uint32_t)(xf((U)(v0[k] & kmask)) >> P.shift) & mask;
+    return pass_digit<LUT>(xf((U)(v0[k] & kmask)), P.shift, mask, lut, lut_shift);
   };
   auto valid = [&](int k) -> bool { return ebase + k * 64 < cnt; };
+  STAMP();  // 1: loads returned
   lds_barrier();  // wc zeroed
 
   uint32_t pos[IT];
-  wlms_rank_fn<IT>(digit, valid, P.bits, &wc[wave][0], pos);
+  wlms_rank_fn<IT>(digit, valid, P.bits, &L.wc[wave][0], pos);
   lds_barrier();
+  STAMP();  // 2: ranked
 
   {  // per-bin totals over waves -> per-wave exclusive offsets; tile scan
+    const uint32_t my_bin = threadIdx.x;
     uint32_t tb = 0;
     if (my_bin < nb) {
 #pragma unroll
       for (int w = 0; w < NW; w++) {
-        const uint32_t c = wc[w][my_bin];
-        wc[w][my_bin] = (uint16_t)tb;
+        const uint32_t c = L.wc[w][my_bin];
+        L.wc[w][my_bin] = (uint16_t)tb;
         tb += c;
       }
     }
     uint32_t tot;
-    const uint32_t ex = block_excl_scan_lds<NT>(tb, scan_sh, &tot);
+    const uint32_t ex = block_excl_scan_lds<NT>(tb, L.scan_sh, &tot);
     if (my_bin < nb) {
-      bin_start[my_bin] = ex;
-      gdst[my_bin] = P.start + my_off - (int64_t)ex;
+      L.bin_start[my_bin] = ex;
+      L.gdst[my_bin] = P.start + my_off - (int64_t)ex;
     }
   }
   lds_barrier();
+  STAMP();  // 3: tile scan
 
 #pragma unroll
   for (int k = 0; k < IT; k++) {
     if (valid(k)) {
       const uint32_t d = digit(k);
-      pos[k] = bin_start[d] + wc[wave][d] + pos[k];
-      sval[pos[k]] = v0[k];
+      pos[k] = L.bin_start[d] + L.wc[wave][d] + pos[k];
+      L.sval[pos[k]] = v0[k];
     }
   }
   lds_barrier();
+  STAMP();  // 4: column 0 staged
 
   // column 0: output slot j's bucket comes from the key itself
   uint16_t dout[IT];
   {
     char* out = desc->cols[0].base[P.dst];
+    const uint32_t w = desc->cols[0].width, st = desc->cols[0].stride;
 #pragma unroll
     for (int i = 0; i < IT; i++) {
       const int j = i * NT + (int)threadIdx.x;
       dout[i] = 0;
       if (j < cnt) {
-        const uint64_t x = sval[j];
-        const uint32_t d = (uint32_t)(xf((U)(x & kmask)) >> P.shift) & mask;
+        const uint64_t x = L.sval[j];
+        const uint32_t d = pass_digit<LUT>(xf((U)(x & kmask)), P.shift, mask, lut, lut_shift);
         dout[i] = (uint16_t)d;
-        store_w(out + ((int64_t)j + gdst[d]) * (int64_t)st0, w0, x);
+        store_w(out + ((int64_t)j + L.gdst[d]) * (int64_t)st, w, x);
       }
     }
   }
-
   for (int c = 1; c < ncols; c++) {
     const uint32_t cw = desc->cols[c].width, cst = desc->cols[c].stride;
     if (c > 1) {
@@ -723,20 +792,62 @@ __global__ __launch_bounds__(kScatterThreads, 4) void scatter_kernel(
 #pragma unroll
       for (int k = 0; k < IT; k++) {
         const int e = ebase + k * 64;
-        v1[k] = e < cnt ? load_w(src + (base + e) * (int64_t)cst, cw) : 0;
+        v1[k] = e < cnt ? load_w(src + (ti.base + e) * (int64_t)cst, cw) : 0;
       }
     }
     lds_barrier();  // every slot of the previous column has been read
 #pragma unroll
     for (int k = 0; k < IT; k++)
-      if (valid(k)) sval[pos[k]] = v1[k];
+      if (valid(k)) L.sval[pos[k]] = v1[k];
     lds_barrier();
     char* out = desc->cols[c].base[P.dst];
 #pragma unroll
     for (int i = 0; i < IT; i++) {
       const int j = i * NT + (int)threadIdx.x;
-      if (j < cnt) store_w(out + ((int64_t)j + gdst[dout[i]]) * (int64_t)cst, cw, sval[j]);
+      if (j < cnt) store_w(out + ((int64_t)j + L.gdst[dout[i]]) * (int64_t)cst, cw, L.sval[j]);
     }
+  }
+  STAMP();  // 5: all stores issued (and, in stamp builds, drained)
+  STAMP_FLUSH(0);
+}
+
+// One tile per workgroup (XCD-aware order).
+template <typename KT, typename U, bool LUT>
+__global__ __launch_bounds__(kScatterThreads, SRS_SCATTER_WAVES_PER_EU) void scatter_kernel(
+    const SortDesc* __restrict__ desc, const SegPlan* __restrict__ plan,
+    const int32_t* __restrict__ tile_seg, const uint64_t* __restrict__ offs) {
+  __shared__ ScatterLds L;
+  const int64_t t = xcd_remap(blockIdx.x, gridDim.x);
+  const int ncols = desc->ncols;
+  uint64_t v0[kScatterItems], v1[kScatterItems];
+  int64_t my_off;
+  const TileInfo ti = scatter_load_tile<KT, U>(desc, plan, tile_seg, offs, t, ncols, v0, v1, my_off);
+  if (ti.cnt == 0) return;
+  scatter_process_tile<KT, U, LUT>(desc, plan, L, ti, ncols, v0, v1, my_off);
+}
+
+// Persistent, software-pipelined: workgroup b owns tiles [b*chunk, (b+1)*chunk).
+template <typename KT, typename U, bool LUT>
+__global__ __launch_bounds__(kScatterThreads, SRS_SCATTER_WAVES_PER_EU) void scatter_pipe_kernel(
+    const SortDesc* __restrict__ desc, const SegPlan* __restrict__ plan,
+    const int32_t* __restrict__ tile_seg, const uint64_t* __restrict__ offs, int64_t ntiles,
+    int64_t chunk) {
+  __shared__ ScatterLds L;
+  const int64_t t0 = (int64_t)blockIdx.x * chunk;
+  const int64_t t1 = min(t0 + chunk, ntiles);
+  if (t0 >= t1) return;
+  const int ncols = desc->ncols;
+  uint64_t a0[kScatterItems], a1[kScatterItems], b0[kScatterItems], b1[kScatterItems];
+  int64_t aoff, boff;
+  TileInfo ta = scatter_load_tile<KT, U>(desc, plan, tile_seg, offs, t0, ncols, a0, a1, aoff);
+  for (int64_t t = t0; t < t1; t += 2) {
+    TileInfo tb;
+    tb.cnt = 0;
+    if (t + 1 < t1) tb = scatter_load_tile<KT, U>(desc, plan, tile_seg, offs, t + 1, ncols, b0, b1, boff);
+    if (ta.cnt > 0) scatter_process_tile<KT, U, LUT>(desc, plan, L, ta, ncols, a0, a1, aoff);
+    if (t + 1 >= t1) break;
+    if (t + 2 < t1) ta = scatter_load_tile<KT, U>(desc, plan, tile_seg, offs, t + 2, ncols, a0, a1, aoff);
+    if (tb.cnt > 0) scatter_process_tile<KT, U, LUT>(desc, plan, L, tb, ncols, b0, b1, boff);
   }
 }
 
@@ -757,8 +868,9 @@ __global__ __launch_bounds__(kScatterThreads, 4) void scatter_kernel(
 //      all varying bits;
 //   4. every column is staged in LDS in input order and written in output
 //      order: coalesced both ways, and safe in place.
-constexpr int kLocalBits = 9;
-constexpr int kRankSortMax = 96;
+constexpr int kLocalBits = 9;      // digit of the LSD fallback passes
+constexpr int kLocalTopBits = 10;  // bucket digit of the fast path
+constexpr int kRankSortMax = 64;   // largest bucket the rank step takes
 
 // Stable ballot-ranked digit pass (fallback path): writes (u, id) in digit
 // order to su / sidx.
@@ -825,17 +937,21 @@ __global__ __launch_bounds__(NT) void local_kernel(const SortDesc* __restrict__ 
   constexpr int IT = kLocalItems;
   constexpr int NW = NT / 64;
   constexpr int CAP = NT * IT;
-  constexpr int NB = 1 << kLocalBits;
+  constexpr int IDXB = CAP <= 4096 ? 12 : 13;  // bits of an index inside the segment
+  static_assert((1 << IDXB) >= CAP, "index bits");
+  constexpr int NB = 1 << kLocalTopBits;
   constexpr int BPT = NB / NT;
-  __shared__ uint64_t sbuf[CAP];          // keys (as U) during the sort, then column staging
-  __shared__ uint16_t sidx[CAP];          // bucket order -> original index
-  __shared__ uint16_t perm[CAP];          // output slot -> original index
-  __shared__ uint32_t hist[NB];           // bucket sizes, then insertion cursors
+  static_assert(BPT >= 1 && BPT * NT == NB, "bins per thread");
+  static_assert(NW * NB == CAP, "ballot counters and the permutation share storage");
+  // sbuf: packed sort words during the sort, column staging afterwards
+  __shared__ uint64_t sbuf[CAP];
+  __shared__ uint16_t wc_perm[CAP];       // ballot counters [NW][NB], then perm[CAP]
+  __shared__ uint32_t bflag[NB];          // bucket holds differing keys
   __shared__ uint32_t bin_start[NB + 1];
   __shared__ uint32_t scan_sh[NW + 1];
   __shared__ unsigned long long sh_or;
   __shared__ int maxlen;
-  U* su = (U*)sbuf;
+  uint16_t* perm = wc_perm;               // output slot -> original index
 
   const Seg g = segs[blockIdx.x];
   const uint32_t wave = threadIdx.x >> 6;
@@ -848,12 +964,15 @@ __global__ __launch_bounds__(NT) void local_kernel(const SortDesc* __restrict__ 
   const int ncols = desc->ncols;
   const int kbytes = desc->key_bits >> 3;
   const uint64_t kmask = kbytes == 8 ? ~0ull : ((1ull << (8 * kbytes)) - 1);
+  STAMP_DECL
+  STAMP();
 
   if (threadIdx.x == 0) {
     sh_or = 0;
     maxlen = 0;
   }
-  for (uint32_t i = threadIdx.x; i < (uint32_t)NB; i += NT) hist[i] = 0;
+  for (uint32_t i = threadIdx.x; i < (uint32_t)CAP; i += NT) wc_perm[i] = 0;
+  for (uint32_t i = threadIdx.x; i < (uint32_t)NB; i += NT) bflag[i] = 0;
 
   // ---- 1. keys (column 0 holds the key in its low bytes) -------------------
   uint64_t v0[IT];
@@ -868,14 +987,14 @@ __global__ __launch_bounds__(NT) void local_kernel(const SortDesc* __restrict__ 
   }
   const U uref = xf((U)(load_w(desc->cols[0].base[g.buf] + base * (int64_t)desc->cols[0].stride,
                                desc->cols[0].width) & kmask));
-  // keys and original indices are recomputed from v0 / the slot when needed
-  // (keeping them in registers costs occupancy)
+  // keys are recomputed from v0 when needed (holding them costs occupancy)
   auto ukey = [&](int k) -> U { return xf((U)(v0[k] & kmask)); };
   auto valid = [&](int k) -> bool { return ebase + k * 64 < cnt; };
   U vor = 0;
 #pragma unroll
   for (int k = 0; k < IT; k++)
     if (valid(k)) vor |= ukey(k) ^ uref;
+  STAMP();  // 1: keys loaded
   if (vor) atomicOr(&sh_or, (unsigned long long)vor);
   lds_barrier();
   const unsigned long long var = sh_or;
@@ -883,101 +1002,127 @@ __global__ __launch_bounds__(NT) void local_kernel(const SortDesc* __restrict__ 
   if (var != 0) {
     const int lo = __ffsll((long long)var) - 1;
     const int hi = 63 - __clzll((long long)var);
-    const int nbits = (hi - lo + 1) < kLocalBits ? (hi - lo + 1) : kLocalBits;
+    // the sort word packs (key bits 0..hi, original index): needs hi+1+IDXB <= 64
+    if (hi + 1 + IDXB > 64) {
+      if (threadIdx.x == 0) fallback[atomicAdd(fallback_count, 1ull)] = g;
+      return;
+    }
+    const int nbits = (hi - lo + 1) < kLocalTopBits ? (hi - lo + 1) : kLocalTopBits;
     const int sh = hi - nbits + 1;
     const uint32_t mask = (1u << nbits) - 1;
-    // ---- 2. bucket pass (LDS atomics) ---------------------------------------
-#pragma unroll
-    for (int k = 0; k < IT; k++)
-      if (valid(k)) atomicAdd(&hist[(uint32_t)(ukey(k) >> sh) & mask], 1u);
+    const uint64_t keep = (hi == 63) ? ~0ull : ((1ull << (hi + 1)) - 1);
+    // ---- 2. stable bucket pass on the top varying bits (ballot ranks) -----
+    auto digit = [&](int k) -> uint32_t { return (uint32_t)(ukey(k) >> sh) & mask; };
+    uint32_t rank[IT];
+    wlms_rank_fn<IT, kLocalTopBits>(digit, valid, nbits, &wc_perm[wave * NB], rank);
     lds_barrier();
     {
       uint32_t tb[BPT], tsum = 0;
 #pragma unroll
       for (int q = 0; q < BPT; q++) {
-        tb[q] = hist[threadIdx.x * BPT + q];
+        const uint32_t b = threadIdx.x * BPT + q;
+        tb[q] = 0;
+#pragma unroll
+        for (int w = 0; w < NW; w++) {
+          const uint32_t c = wc_perm[w * NB + b];
+          wc_perm[w * NB + b] = (uint16_t)tb[q];
+          tb[q] += c;
+        }
         tsum += tb[q];
       }
       uint32_t tot;
       uint32_t ex = block_excl_scan_lds<NT>(tsum, scan_sh, &tot);
-      int mymax = 0;
 #pragma unroll
       for (int q = 0; q < BPT; q++) {
         bin_start[threadIdx.x * BPT + q] = ex;
-        hist[threadIdx.x * BPT + q] = ex;  // becomes the insertion cursor
         ex += tb[q];
-        mymax = (int)tb[q] > mymax ? (int)tb[q] : mymax;
       }
       if (threadIdx.x == 0) bin_start[NB] = tot;
+    }
+    lds_barrier();
+#pragma unroll
+    for (int k = 0; k < IT; k++) {
+      if (valid(k)) {
+        const uint32_t d = digit(k);
+        const uint32_t p = bin_start[d] + wc_perm[wave * NB + d] + rank[k];
+        sbuf[p] = (((uint64_t)ukey(k) & keep) << IDXB) | (uint64_t)(ebase + k * 64);
+      }
+    }
+    lds_barrier();
+    STAMP();  // 2: stable bucket pass
+    // ---- 3. buckets whose keys all equal are final (the pass was stable) --
+#pragma unroll
+    for (int i = 0; i < IT; i++) {
+      const int p = i * NT + (int)threadIdx.x;
+      if (p < cnt) {
+        const uint64_t x = sbuf[p];
+        const uint32_t d = (uint32_t)(x >> (sh + IDXB)) & mask;
+        if (((x ^ sbuf[bin_start[d]]) >> IDXB) != 0) bflag[d] = 1;
+      }
+    }
+    lds_barrier();
+    {
+      int mymax = 0;
+#pragma unroll
+      for (int q = 0; q < BPT; q++) {
+        const uint32_t b = threadIdx.x * BPT + q;
+        const int len = (int)(bin_start[b + 1] - bin_start[b]);
+        if (bflag[b] && len > mymax) mymax = len;
+      }
       if (mymax > 0) atomicMax(&maxlen, mymax);
     }
     lds_barrier();
-    const int mlen = maxlen;
-    if (mlen <= kRankSortMax) {
+    STAMP();  // 3: bucket flags
+    if (maxlen > kRankSortMax) {
+      // a large bucket of differing keys: local_lsd_kernel takes the segment
+      // (nothing has been written to global memory yet)
+      if (threadIdx.x == 0) fallback[atomicAdd(fallback_count, 1ull)] = g;
+      return;
+    }
+    // ---- 4. rank inside mixed buckets: #(words of the bucket below mine) --
+    // The word orders by (key, original index): stable. Slots in two halves
+    // bound register use; a wave-uniform trip count keeps LDS reads in flight.
+    constexpr int H = IT / 2;
 #pragma unroll
-      for (int k = 0; k < IT; k++) {
-        if (valid(k)) {
-          const U uk = ukey(k);
-          const uint32_t p = atomicAdd(&hist[(uint32_t)(uk >> sh) & mask], 1u);
-          su[p] = uk;
-          sidx[p] = (uint16_t)(ebase + k * 64);
-        }
-      }
-      lds_barrier();
-      // ---- 3. rank inside each bucket by (key, original index) -------------
-      // (slots in two halves to bound register use; results go straight to
-      // perm, a different array than the one being read)
-      constexpr int H = IT / 2;
+    for (int half = 0; half < 2; half++) {
+      uint64_t x[H];
+      uint32_t bs[H], bl[H], r[H];
+      int wmax = 0;
 #pragma unroll
-      for (int half = 0; half < 2; half++) {
-        U x[H];
-        uint32_t bs[H], bl[H], xid[H], r[H];
-        int wmax = 0;
-#pragma unroll
-        for (int i = 0; i < H; i++) {
-          const int p = (half * H + i) * NT + (int)threadIdx.x;
-          bl[i] = 0;
-          bs[i] = 0;
-          x[i] = 0;
-          xid[i] = 0;
-          r[i] = 0;
-          if (p < cnt) {
-            x[i] = su[p];
-            xid[i] = sidx[p];
-            const uint32_t d = (uint32_t)(x[i] >> sh) & mask;
+      for (int i = 0; i < H; i++) {
+        const int p = (half * H + i) * NT + (int)threadIdx.x;
+        bl[i] = 0;
+        bs[i] = (uint32_t)p;
+        x[i] = 0;
+        r[i] = 0;
+        if (p < cnt) {
+          x[i] = sbuf[p];
+          const uint32_t d = (uint32_t)(x[i] >> (sh + IDXB)) & mask;
+          if (bflag[d]) {
             bs[i] = bin_start[d];
             bl[i] = bin_start[d + 1] - bs[i];
             wmax = (int)bl[i] > wmax ? (int)bl[i] : wmax;
           }
         }
-#pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) {
-          const int t2 = __shfl_xor(wmax, o, 64);
-          wmax = t2 > wmax ? t2 : wmax;
-        }
-        for (int j = 0; j < wmax; j++) {
-#pragma unroll
-          for (int i = 0; i < H; i++) {
-            if ((uint32_t)j < bl[i]) {
-              const U y = su[bs[i] + j];
-              const uint32_t yid = sidx[bs[i] + j];
-              r[i] += (y < x[i]) | ((y == x[i]) & (yid < xid[i]));
-            }
-          }
-        }
-#pragma unroll
-        for (int i = 0; i < H; i++) {
-          const int p = (half * H + i) * NT + (int)threadIdx.x;
-          if (p < cnt) perm[r[i] + bs[i]] = (uint16_t)xid[i];
-        }
       }
-      lds_barrier();
-    } else {
-      // skewed bucket sizes: hand the segment to local_lsd_kernel (nothing
-      // has been written to global memory yet)
-      if (threadIdx.x == 0) fallback[atomicAdd(fallback_count, 1ull)] = g;
-      return;
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) {
+        const int t2 = __shfl_xor(wmax, o, 64);
+        wmax = t2 > wmax ? t2 : wmax;
+      }
+      for (int j = 0; j < wmax; j++) {
+#pragma unroll
+        for (int i = 0; i < H; i++)
+          if ((uint32_t)j < bl[i]) r[i] += sbuf[bs[i] + j] < x[i];
+      }
+#pragma unroll
+      for (int i = 0; i < H; i++) {
+        const int p = (half * H + i) * NT + (int)threadIdx.x;
+        if (p < cnt) perm[bs[i] + r[i]] = (uint16_t)(x[i] & ((1u << IDXB) - 1));
+      }
     }
+    lds_barrier();
+    STAMP();  // 4: ranked
   } else if (g.buf == BUF_OUT) {
     return;  // all keys equal and already home
   } else {
@@ -990,19 +1135,23 @@ __global__ __launch_bounds__(NT) void local_kernel(const SortDesc* __restrict__ 
 #pragma unroll
   for (int k = 0; k < IT; k++) id[k] = perm[ebase + k * 64];
 
-  // ---- 4. columns: stage in input order, write in output order --------------
-  // (column 0 is re-read from L2 rather than held in registers through the
-  // sort; in place is safe: every load of a column completes before the
-  // barrier that precedes its stores)
+  // ---- 5. columns: stage in input order, write in output order --------------
+  // (in place is safe: every load of a column completes before the barrier
+  // that precedes its stores)
   for (int c = 0; c < ncols; c++) {
     const char* src = desc->cols[c].base[g.buf];
     char* out = desc->cols[c].base[BUF_OUT];
     const uint32_t w = desc->cols[c].width, st = desc->cols[c].stride;
     uint64_t v[IT];
+    if (SRS_LOCAL_KEEP_KEYS && c == 0) {
 #pragma unroll
-    for (int k = 0; k < IT; k++) {
-      const int e = ebase + k * 64;
-      v[k] = e < cnt ? load_w(src + (base + e) * (int64_t)st, w) : 0;
+      for (int k = 0; k < IT; k++) v[k] = v0[k];
+    } else {
+#pragma unroll
+      for (int k = 0; k < IT; k++) {
+        const int e = ebase + k * 64;
+        v[k] = e < cnt ? load_w(src + (base + e) * (int64_t)st, w) : 0;
+      }
     }
     lds_barrier();  // previous users of sbuf are done
 #pragma unroll
@@ -1014,7 +1163,9 @@ __global__ __launch_bounds__(NT) void local_kernel(const SortDesc* __restrict__ 
       const int e = ebase + k * 64;
       if (valid(k)) store_w(out + (base + e) * (int64_t)st, w, sbuf[id[k]]);
     }
+    STAMP();  // 5, 6: column moved (loads, staging, stores drained)
   }
+  STAMP_FLUSH(1);
 }
 
 // Fallback for segments whose top-digit buckets are too large for the rank
@@ -1162,10 +1313,10 @@ __global__ void fill_kernel(int64_t n, int kind, uint64_t seed, uint64_t first,
   }
 
 void launch_plan(const Seg* big, int64_t nbig, SegPlan* plan, int64_t* tcount,
-                 int64_t* gcount, unsigned long long* var_or, uint64_t* elems,
+                 int64_t* gcount, unsigned long long* var_or, uint64_t* elems, int force_bits,
                  hipStream_t st) {
   plan_kernel<<<(unsigned)((nbig + 255) / 256), 256, 0, st>>>(big, nbig, plan, tcount,
-                                                              gcount, var_or, elems);
+                                                              gcount, var_or, elems, force_bits);
 }
 
 void launch_plan_bases(SegPlan* plan, int64_t nbig, const int64_t* tbase,
@@ -1182,10 +1333,14 @@ void launch_seg_map(const int64_t* bases, int64_t nbig, int64_t n, int32_t* out,
 
 void launch_count(int key_size, const SortDesc* d, const SegPlan* plan,
                   const int32_t* tile_seg, int64_t ntiles, uint32_t* hist,
-                  unsigned long long* var_or, hipStream_t st) {
-#define CALL(KT, U)                                                                  \
-  count_kernel<KT, U><<<(unsigned)ntiles, kScatterThreads, 0, st>>>(d, plan, tile_seg, \
-                                                                    hist, var_or)
+                  unsigned long long* var_or, bool lut, hipStream_t st) {
+#define CALL(KT, U)                                                                        \
+  if (lut)                                                                                 \
+    count_kernel<KT, U, true><<<(unsigned)ntiles, kScatterThreads, 0, st>>>(d, plan, tile_seg, \
+                                                                          hist, var_or);   \
+  else                                                                                     \
+    count_kernel<KT, U, false><<<(unsigned)ntiles, kScatterThreads, 0, st>>>(d, plan, tile_seg, \
+                                                                           hist, var_or)
   SRS_KEY_DISPATCH(key_size, CALL)
 #undef CALL
 }
@@ -1212,10 +1367,31 @@ void launch_offsets(SegPlan* plan, int64_t nbig, const int32_t* group_seg, int64
 }
 
 void launch_scatter(int key_size, const SortDesc* d, const SegPlan* plan,
-                    const int32_t* tile_seg, const uint64_t* offs, int64_t ntiles,
+                    const int32_t* tile_seg, const uint64_t* offs, int64_t ntiles, bool lut,
                     hipStream_t st) {
-#define CALL(KT, U) \
-  scatter_kernel<KT, U><<<(unsigned)ntiles, kScatterThreads, 0, st>>>(d, plan, tile_seg, offs)
+#if SRS_SCATTER_PIPE
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) == hipSuccess)
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  const int64_t nwg = std::min<int64_t>(ntiles, (int64_t)cus * SRS_SCATTER_WG_PER_CU);
+  const int64_t chunk = (ntiles + nwg - 1) / nwg;
+  const int64_t grid = (ntiles + chunk - 1) / chunk;
+#define CALL(KT, U)                                                                        \
+  if (lut)                                                                                 \
+    scatter_pipe_kernel<KT, U, true><<<(unsigned)grid, kScatterThreads, 0, st>>>(          \
+        d, plan, tile_seg, offs, ntiles, chunk);                                           \
+  else                                                                                     \
+    scatter_pipe_kernel<KT, U, false><<<(unsigned)grid, kScatterThreads, 0, st>>>(         \
+        d, plan, tile_seg, offs, ntiles, chunk)
+#else
+#define CALL(KT, U)                                                                         \
+  if (lut)                                                                                  \
+    scatter_kernel<KT, U, true><<<(unsigned)ntiles, kScatterThreads, 0, st>>>(d, plan, tile_seg, \
+                                                                            offs);          \
+  else                                                                                      \
+    scatter_kernel<KT, U, false><<<(unsigned)ntiles, kScatterThreads, 0, st>>>(d, plan,       \
+                                                                             tile_seg, offs)
+#endif
   SRS_KEY_DISPATCH(key_size, CALL)
 #undef CALL
 }
@@ -1249,6 +1425,33 @@ void launch_fill(int64_t n, int kind, uint64_t seed, uint64_t first, void* keys,
 }  // namespace srs
 
 namespace srs {
+
+// Histogram of the transformed top `bits` bits (multi-GPU shard split).
+template <typename KT, typename U>
+__global__ __launch_bounds__(256) void key_hist_kernel(int64_t n, const KT* __restrict__ keys,
+                                                       SortDesc d, int bits,
+                                                       unsigned long long* __restrict__ hist) {
+  __shared__ uint32_t h[1 << kHistMaxBits];
+  const int nb = 1 << bits;
+  const int shift = d.key_bits - bits;
+  Xform<U> xf;
+  xf.init(d);
+  for (int i = threadIdx.x; i < nb; i += 256) h[i] = 0;
+  __syncthreads();
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+    atomicAdd(&h[(uint32_t)(xf((U)keys[i]) >> shift)], 1u);
+  __syncthreads();
+  for (int i = threadIdx.x; i < nb; i += 256)
+    if (h[i]) atomicAdd(&hist[i], (unsigned long long)h[i]);
+}
+
+void launch_key_hist(int key_size, int64_t n, const void* keys, const SortDesc& d, int bits,
+                     unsigned long long* hist, hipStream_t st) {
+  const int grid = (int)std::min<int64_t>(2048, (n + 255) / 256);
+#define CALL(KT, U) key_hist_kernel<KT, U><<<grid, 256, 0, st>>>(n, (const KT*)keys, d, bits, hist)
+  SRS_KEY_DISPATCH(key_size, CALL)
+#undef CALL
+}
 
 // Kernel arguments are captured at launch, so the descriptor needs no pinned
 // staging buffer and is safe to rebuild for the next call immediately.

@@ -27,7 +27,7 @@ except Exception:  # pragma: no cover - torch is present in this image
     _HAVE_TORCH = False
 
 _PKG_ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-LIB_PATH = os.path.join(_PKG_ROOT, "lib", "libsrs_amd.so")
+LIB_PATH = os.environ.get("SRS_AMD_LIB") or os.path.join(_PKG_ROOT, "lib", "libsrs_amd.so")
 
 # srs_key_kind (include/srs_c_api.h)
 KEY_U8, KEY_I8, KEY_U16, KEY_I16, KEY_U32, KEY_I32, KEY_U64, KEY_I64, KEY_F32, KEY_F64 = range(10)
@@ -63,6 +63,10 @@ def lib() -> ctypes.CDLL:
     L.srs_sort_aos_device.argtypes = [i64, ctypes.c_int, ctypes.c_int, i64, vp, u32, vp, vp]
     L.srs_fill_synthetic_device.argtypes = [i64, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64,
                                             vp, i32, vp, vp, vp]
+    L.srs_key_histogram_device.argtypes = [i64, ctypes.c_int, ctypes.c_int, vp, ctypes.c_int, vp,
+                                           vp]
+    L.srs_partition_device.argtypes = [i64, ctypes.c_int, ctypes.c_int, vp, i32, vp, vp,
+                                       ctypes.c_int, vp, i32, vp, vp, vp, vp]
     L.srs_last_error.restype = ctypes.c_char_p
     L.srs_version.restype = ctypes.c_char_p
     L.srs_set_kernel_timing.argtypes = [ctypes.c_int]
@@ -207,6 +211,38 @@ def fill_synthetic_device(keys, *payloads, seed: int = 42 << 32, first_index: in
                                            _ptr_array([p.data_ptr() for p in payloads]),
                                            _size_array([p.element_size() for p in payloads]),
                                            _stream_ptr(stream)))
+
+
+# --------------------------------------------------------------------------
+# multi-GPU shard primitives (see srs_amd.dist)
+# --------------------------------------------------------------------------
+def key_histogram_device(keys, hist, bits: int, up: bool = True, key_kind: int | None = None,
+                         stream=None) -> None:
+    """Adds the histogram of the transformed top `bits` key bits into `hist`
+    (int64 device tensor of 2^bits entries)."""
+    kind = _torch_kind(keys) if key_kind is None else int(key_kind)
+    if hist.numel() != (1 << bits) or hist.element_size() != 8 or not hist.is_cuda:
+        raise ValueError("hist must be a device tensor of 2^bits 64-bit counters")
+    _check(lib().srs_key_histogram_device(keys.numel(), kind, int(bool(up)), keys.data_ptr(),
+                                          int(bits), hist.data_ptr(), _stream_ptr(stream)))
+
+
+def partition_device(keys, payloads, bits: int, part_of_bucket, num_parts: int, out,
+                     up: bool = True, key_kind: int | None = None, stream=None):
+    """Stable partition by destination group (srs_partition_device).
+    `part_of_bucket`: int32 device tensor of 2^bits entries. `out` =
+    (keys_out, *payloads_out). Returns the host list of group sizes."""
+    kind = _torch_kind(keys) if key_kind is None else int(key_kind)
+    if part_of_bucket.dtype.itemsize != 4 or part_of_bucket.numel() != (1 << bits):
+        raise ValueError("part_of_bucket must hold 2^bits int32 entries")
+    counts = (ctypes.c_int64 * num_parts)()
+    pays = list(payloads)
+    _check(lib().srs_partition_device(
+        keys.numel(), kind, int(bool(up)), keys.data_ptr(), len(pays),
+        _ptr_array([p.data_ptr() for p in pays]), _size_array([p.element_size() for p in pays]),
+        int(bits), part_of_bucket.data_ptr(), int(num_parts), out[0].data_ptr(),
+        _ptr_array([o.data_ptr() for o in out[1:]]), counts, _stream_ptr(stream)))
+    return [int(c) for c in counts]
 
 
 # --------------------------------------------------------------------------

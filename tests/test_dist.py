@@ -1,0 +1,149 @@
+"""Multi-process tests of the top-radix-bits shard protocol (srs_amd.dist)
+on CPU with the gloo backend, world_size 2 and 3. The device kernels are
+replaced by a numpy backend that follows the same contracts (stable
+partition by a bucket -> rank table; stable sort in the reference key order);
+the GPU kernels themselves are covered by the -m gpu tests."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from srs_testlib import KIND_UINT, key_size, transformed_keys
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+class NumpyShardOps:
+    """CPU stand-in for HipShardOps with the same contracts."""
+
+    def __init__(self, kind):
+        self.kind = kind
+
+    def _u(self, keys):
+        return transformed_keys(self.kind, True, keys.numpy())
+
+    def histogram(self, keys, bits):
+        top = self._u(keys) >> np.uint64(8 * key_size(self.kind) - bits)
+        return torch.from_numpy(np.bincount(top.astype(np.int64), minlength=1 << bits)
+                                .astype(np.int64))
+
+    def partition(self, keys, pays, bits, part_of_bucket, nparts, out):
+        top = (self._u(keys) >> np.uint64(8 * key_size(self.kind) - bits)).astype(np.int64)
+        dest = part_of_bucket.numpy()[top]
+        order = np.argsort(dest, kind="stable")
+        out[0][:len(order)] = keys[torch.from_numpy(order)]
+        for o, p in zip(out[1:], pays):
+            o[:len(order)] = p[torch.from_numpy(order)]
+        return np.bincount(dest, minlength=nparts).tolist()
+
+    def sort(self, keys, pays):
+        order = torch.from_numpy(np.argsort(self._u(keys), kind="stable"))
+        keys.copy_(keys[order])
+        for p in pays:
+            p.copy_(p[order])
+
+
+def _worker(rank, world, port, kind, n_per, dist_kind, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "simd-radix-sort_amd",
+                                    "python"))
+    from srs_amd.dist import ShardSorter
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        _run(rank, world, kind, n_per, dist_kind, q)
+    except Exception as e:  # report instead of hanging the parent
+        q.put(("error", repr(e)))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+def _run(rank, world, kind, n_per, dist_kind, q):
+    from srs_amd.dist import ShardSorter
+    if True:
+        rng = np.random.default_rng(100 + rank)
+        ut = KIND_UINT[kind]
+        n = n_per + rank * 17  # ragged shard sizes
+        if dist_kind == "uniform":
+            k = rng.integers(0, 2**63, n, dtype=np.uint64).astype(ut)
+        elif dist_kind == "skewed":  # everything in a few top buckets
+            k = (rng.integers(0, 3, n, dtype=np.uint64) << np.uint64(8 * key_size(kind) - 3)
+                 | rng.integers(0, 1000, n, dtype=np.uint64)).astype(ut)
+        else:  # all equal
+            k = np.full(n, 7, dtype=ut)
+        keys = torch.from_numpy(k.copy())
+        pay = torch.from_numpy(np.arange(n, dtype=np.int64) + rank * 10**9)
+        sorter = ShardSorter(NumpyShardOps(kind), n, [torch.int64], keys.dtype, "cpu", bits=8)
+        ok, (op,) = sorter.sort(keys, [pay])
+        mine = ok.numpy().copy()
+        u = transformed_keys(kind, True, mine)
+        sorted_ok = bool(np.all(u[1:] >= u[:-1]))
+        # boundary check with the next rank, and a multiset check on rank 0
+        lohi = torch.tensor([int(u[0]) if len(u) else -1, int(u[-1]) if len(u) else -1],
+                            dtype=torch.float64)
+        allb = [torch.zeros(2, dtype=torch.float64) for _ in range(world)]
+        dist.all_gather(allb, lohi)
+        gathered_k = [None] * world
+        gathered_p = [None] * world
+        dist.all_gather_object(gathered_k, mine.tolist())
+        dist.all_gather_object(gathered_p, op.numpy().tolist())
+        inputs = [None] * world
+        dist.all_gather_object(inputs, (k.tolist(), pay.numpy().tolist()))
+        if rank == 0:
+            outk = np.concatenate([np.array(g, dtype=ut) for g in gathered_k])
+            outp = np.concatenate([np.array(g, dtype=np.int64) for g in gathered_p])
+            ink = np.concatenate([np.array(i[0], dtype=ut) for i in inputs])
+            inp = np.concatenate([np.array(i[1], dtype=np.int64) for i in inputs])
+            ref = np.argsort(transformed_keys(kind, True, ink), kind="stable")
+            q.put((sorted_ok, np.array_equal(outk, ink[ref]),
+                   sorted(zip(outk.tolist(), outp.tolist())) ==
+                   sorted(zip(ink.tolist(), inp.tolist())),
+                   [b.tolist() for b in allb]))
+        else:
+            q.put((sorted_ok, True, True, None))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("dist_kind", ["uniform", "skewed", "equal"])
+def test_shard_sort_gloo(world, dist_kind):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, 6, 3000, dist_kind, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert not [r for r in res if r[0] == "error"], res
+    for sorted_ok, keys_ok, multiset_ok, bounds in res:
+        assert sorted_ok and keys_ok and multiset_ok
+    b = [r[3] for r in res if r[3] is not None][0]
+    nonempty = [x for x in b if x[0] >= 0]
+    for a, c in zip(nonempty, nonempty[1:]):
+        assert a[1] <= c[0]  # last key of rank r <= first key of rank r+1
+
+
+def test_balanced_split_is_monotone_and_balanced():
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "simd-radix-sort_amd",
+                                    "python"))
+    from srs_amd.dist import balanced_split
+    h = torch.tensor([5, 0, 100, 3, 3, 3, 50, 0, 0, 36], dtype=torch.int64)
+    for w in (1, 2, 3, 8):
+        p = balanced_split(h, w)
+        assert p.dtype == torch.int32 and len(p) == len(h)
+        assert bool((p[1:] >= p[:-1]).all()) and int(p.min()) >= 0 and int(p.max()) < w
+    u = balanced_split(torch.full((256,), 10, dtype=torch.int64), 8)
+    assert torch.bincount(u.long(), minlength=8).tolist() == [32] * 8

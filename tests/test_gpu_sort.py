@@ -266,3 +266,34 @@ def test_errors_are_loud():
         srs_amd.sort_combined(np.zeros((10, 12), np.uint8), srs_amd.KEY_U32)  # not a power of two
     with pytest.raises(TypeError):
         srs_amd.sort(np.zeros(10, np.complex64))
+
+
+# ---------------------------------------------------------------------------
+# multi-GPU shard primitives on one GPU
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("kind", [4, 6, 7, 8, 9], ids=lambda k: KIND_NAMES[k])
+def test_key_histogram_and_partition(kind):
+    torch = _torch()
+    from srs_amd.dist import balanced_split
+    n = 1_000_003
+    keys_h = make_keys(kind, "gaussian" if kind in (7, 9) else "uniform", n, kind)
+    pay_h = np.arange(n, dtype=np.int64)
+    tdt = {4: torch.int32, 6: torch.int64, 7: torch.int64, 8: torch.float32, 9: torch.float64}
+    keys = torch.from_numpy(keys_h.view(np.int32 if kind == 4 else np.int64)
+                            if kind in (4, 6) else keys_h).cuda()
+    pay = torch.from_numpy(pay_h).cuda()
+    bits = 10
+    hist = torch.zeros(1 << bits, dtype=torch.int64, device="cuda")
+    srs_amd.key_histogram_device(keys, hist, bits, key_kind=kind)
+    u = transformed_keys(kind, True, keys_h)
+    top = (u >> np.uint64(8 * key_size(kind) - bits)).astype(np.int64)
+    assert np.array_equal(hist.cpu().numpy(), np.bincount(top, minlength=1 << bits))
+    for world in (1, 3, 8):
+        pob = balanced_split(hist, world)
+        ko, po = torch.empty_like(keys), torch.empty_like(pay)
+        counts = srs_amd.partition_device(keys, [pay], bits, pob, world, (ko, po), key_kind=kind)
+        dest = pob.cpu().numpy()[top]
+        assert counts == np.bincount(dest, minlength=world).tolist()
+        order = np.argsort(dest, kind="stable")  # stable partition
+        assert bytes_equal(ko.cpu().numpy(), keys.cpu().numpy()[order])
+        assert bytes_equal(po.cpu().numpy(), pay_h[order])

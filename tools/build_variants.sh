@@ -1,0 +1,16 @@
+#!/bin/bash
+# Build tuning variants of libsrs_amd.so into simd-radix-sort_amd/lib/variants/<name>/.
+# usage: tools/build_variants.sh name:"-DFOO=1 -DBAR=2" ...
+set -e
+cd "$(dirname "$0")/../simd-radix-sort_amd"
+for spec in "$@"; do
+  name=${spec%%:*}; flags=${spec#*:}
+  out=lib/variants/$name; mkdir -p $out build/v_$name
+  for f in srs_kernels srs_api; do
+    /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -munsafe-fp-atomics $flags \
+      -c csrc/$f.hip -o build/v_$name/$f.o &
+  done
+  wait
+  /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o $out/libsrs_amd.so build/v_$name/*.o -Wl,-rpath,/opt/rocm/lib
+  echo "built $name ($flags)"
+done
