@@ -200,7 +200,8 @@ def main():
 
     # ---- per-kernel device time (HIP events on the launch stream) ----------
     kstats = {}
-    for name in ("count", "scatter", "local", "scan", "plan", "children", "copy"):
+    for name in ("count", "scatter", "local", "local_fast", "local_stable", "local_lsd", "scan",
+                 "plan", "children", "copy"):
         l, ms, el = srs_amd.kernel_stats(name)
         if l:
             kstats[name] = {"launches": l, "ms": ms, "elems": el}

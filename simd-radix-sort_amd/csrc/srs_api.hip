@@ -112,6 +112,11 @@ struct TimedScope {
   }
 };
 
+bool timing_enabled() {
+  std::lock_guard<std::mutex> lk(g_tmu);
+  return g_timing;
+}
+
 void note_elems(const char* name, double elems) {
   std::lock_guard<std::mutex> lk(g_tmu);
   if (g_timing) g_stats[name].elems += elems;
@@ -174,7 +179,7 @@ struct Workspace {
   DevBuf tmp;         // TMP data buffer (same footprint as the input)
   DevBuf stage;       // device copy of host arrays (host-pointer API)
   DevBuf desc;        // SortDesc
-  DevBuf big[2], local, local2, copy, fallback;
+  DevBuf big[2], local, local2, copy, fallback, fallback2;
   DevBuf plan, tcount, gcount, tbase, gbase, var, sbase;
   DevBuf tile_seg, group_seg, hist, offs, gsum, gofs, scan_tmp, totals, ctr;
   ListCounters* h_ctr = nullptr;
@@ -421,12 +426,45 @@ int run_sort(Workspace* W, const Request& R, hipStream_t st) {
   if (n_local + n_local2 > 0) {
     note_elems("local", (double)W->h_ctr->local_elems);
     TimedScope ts("local", (double)0, st);
+    // fast kernel -> (large buckets) stable kernel -> (wide keys) LSD kernel;
+    // the fallback kernels read their list lengths on device
     SRS_TRY(ensure(W->fallback, (n_local + n_local2) * sizeof(Seg)));
-    Seg* fb = (Seg*)W->fallback.p;
+    SRS_TRY(ensure(W->fallback2, (n_local + n_local2) * sizeof(Seg)));
+    Seg* fb = (Seg*)W->fallback.p;         // [0, n_local2): large, then small
+    Seg* fb1 = fb + n_local2;
+    Seg* fb2 = (Seg*)W->fallback2.p;
     unsigned long long* nfb = &d_ctr->n_fallback;
-    if (n_local2 > 0) launch_local(ks, d_desc, (Seg*)W->local2.p, n_local2, 1, fb, nfb, st);
-    if (n_local > 0) launch_local(ks, d_desc, (Seg*)W->local.p, n_local, 0, fb, nfb, st);
-    launch_local_lsd(ks, d_desc, fb, nfb, (int)std::min<int64_t>(1024, n_local + n_local2), st);
+    unsigned long long* nfb1 = &d_ctr->n_fallback1;
+    unsigned long long* nfb2 = &d_ctr->n_fallback2;
+    {
+      TimedScope ts1("local_fast", 0, st);
+      if (n_local2 > 0) launch_local(ks, d_desc, (Seg*)W->local2.p, n_local2, 1, fb, nfb, st);
+      if (n_local > 0) launch_local(ks, d_desc, (Seg*)W->local.p, n_local, 0, fb1, nfb1, st);
+    }
+    {
+      TimedScope ts2("local_stable", 0, st);
+      // one workgroup per listed segment up to a cap (the list length is
+      // only known on device; surplus workgroups exit at once)
+      if (n_local2 > 0)
+        launch_local_stable(ks, d_desc, fb, nfb, 1, fb2, nfb2,
+                            (int)std::min<int64_t>(SRS_STABLE_GRID_MAX, n_local2), st);
+      if (n_local > 0)
+        launch_local_stable(ks, d_desc, fb1, nfb1, 0, fb2, nfb2,
+                            (int)std::min<int64_t>(SRS_STABLE_GRID_MAX, n_local), st);
+    }
+    {
+      TimedScope ts3("local_lsd", 0, st);
+      const int fgrid = (int)std::min<int64_t>(512, n_local + n_local2);
+      launch_local_lsd(ks, d_desc, fb2, nfb2, fgrid, st);
+    }
+    if (timing_enabled()) {
+      // diagnostics: how many segments took each fallback
+      ListCounters c;
+      HIP_TRY(hipMemcpyAsync(&c, d_ctr, sizeof(c), hipMemcpyDeviceToHost, st));
+      HIP_TRY(hipStreamSynchronize(st));
+      note_elems("local_stable", (double)(c.n_fallback + c.n_fallback1));
+      note_elems("local_lsd", (double)c.n_fallback2);
+    }
   }
   if (n_copy > 0) {
     std::vector<Seg> cp((size_t)n_copy);
@@ -784,7 +822,7 @@ int srs_release_workspace(void) {
   std::lock_guard<std::mutex> lk(g_wmu);
   for (auto& kv : g_ws) {
     Workspace* w = kv.second;
-    DevBuf* bufs[] = {&w->tmp, &w->stage, &w->desc, &w->big[0], &w->big[1], &w->local, &w->local2, &w->fallback,
+    DevBuf* bufs[] = {&w->tmp, &w->stage, &w->desc, &w->big[0], &w->big[1], &w->local, &w->local2, &w->fallback, &w->fallback2,
                       &w->copy, &w->plan, &w->tcount, &w->gcount, &w->tbase, &w->gbase,
                       &w->var, &w->sbase, &w->tile_seg, &w->group_seg, &w->hist, &w->offs,
                       &w->gsum, &w->gofs, &w->scan_tmp, &w->totals, &w->ctr};

@@ -75,16 +75,18 @@ struct ListCounters {
   unsigned long long n_copy;   // finished segments that must be copied to OUT
   unsigned long long local_elems;  // keys in the local lists (timing stats)
   unsigned long long n_local2; // segments for the large-class LDS sort
-  unsigned long long n_fallback;  // segments handed to the LSD fallback kernel
+  unsigned long long n_fallback;  // large-class segments handed to the stable kernel
+  unsigned long long n_fallback1; // small-class segments handed to the stable kernel
+  unsigned long long n_fallback2; // segments handed on to the LSD local kernel
 };
 
 // Tuning constants (see DESIGN.md §4 for how they were chosen).
 // (overridable at build time for tuning sweeps: tools/build_variants.sh)
 #ifndef SRS_SCATTER_THREADS
-#define SRS_SCATTER_THREADS 512
+#define SRS_SCATTER_THREADS 1024
 #endif
 #ifndef SRS_SCATTER_ITEMS
-#define SRS_SCATTER_ITEMS 8
+#define SRS_SCATTER_ITEMS 4
 #endif
 #ifndef SRS_SCATTER_WAVES_PER_EU
 #define SRS_SCATTER_WAVES_PER_EU 4
@@ -96,21 +98,44 @@ struct ListCounters {
 #define SRS_SCATTER_WG_PER_CU 2
 #endif
 #ifndef SRS_LOCAL_KEEP_KEYS
-#define SRS_LOCAL_KEEP_KEYS 1
+#define SRS_LOCAL_KEEP_KEYS 0
 #endif
 constexpr int kScatterThreads = SRS_SCATTER_THREADS;
 constexpr int kScatterItems = SRS_SCATTER_ITEMS;
 constexpr int kTile = kScatterThreads * kScatterItems;   // keys per tile
+#ifndef SRS_COUNT_THREADS
+#define SRS_COUNT_THREADS 256
+#endif
+constexpr int kCountThreads = SRS_COUNT_THREADS;         // count kernel: one tile per block
+constexpr int kCountItems = kTile / kCountThreads;
+static_assert(kCountItems * kCountThreads == kTile, "count block shape");
 constexpr int kMaxDigitBits = 9;
 constexpr int kMaxBins = 1 << kMaxDigitBits;   // histogram row stride (tile-major)
 constexpr int kScanGroup = 256;                 // tiles per column-scan group
 constexpr int kHistMaxBits = 12;                // srs_key_histogram_device
 
-constexpr int kLocalItems = 16;
-constexpr int kLocalThreads = 512;
+// local sort classes: fast kernel (atomic bucket pass + rank) in two sizes,
+// then the stable kernel and the LSD kernel as fallbacks (same capacity as
+// the large class)
+#ifndef SRS_LOCAL_THREADS
+#define SRS_LOCAL_THREADS 1024
+#endif
+#ifndef SRS_LOCAL_ITEMS
+#define SRS_LOCAL_ITEMS 8
+#endif
+#ifndef SRS_STABLE_GRID_MAX
+#define SRS_STABLE_GRID_MAX (1 << 30)
+#endif
+constexpr int kLocalItems = SRS_LOCAL_ITEMS;
+constexpr int kLocalThreads = SRS_LOCAL_THREADS;
 constexpr int kLocalCap = kLocalThreads * kLocalItems;    // 8192 keys per segment
-constexpr int kLocalThreadsSmall = 256;
-constexpr int kLocalCapSmall = kLocalThreadsSmall * kLocalItems;  // 4096
+constexpr int kLocalItemsSmall = 8;
+constexpr int kLocalThreadsSmall = 512;
+constexpr int kLocalCapSmall = kLocalThreadsSmall * kLocalItemsSmall;  // 4096
+constexpr int kLocalStableThreads = 512;
+constexpr int kLocalStableItems = 16;
+static_assert(kLocalStableThreads * kLocalStableItems == kLocalCap, "fallback capacity");
+static_assert(kLocalStableThreads / 2 * kLocalStableItems == kLocalCapSmall, "fallback capacity");
 constexpr int kLocalTarget = 6144;                        // digit sizing target
 
 }  // namespace srs

@@ -32,6 +32,9 @@ void launch_key_hist(int key_size, int64_t n, const void* keys, const SortDesc& 
                      unsigned long long* hist, hipStream_t st);
 void launch_local(int key_size, const SortDesc* d, const Seg* segs, int64_t nsegs, int big_class,
                   Seg* fallback, unsigned long long* fallback_count, hipStream_t st);
+void launch_local_stable(int key_size, const SortDesc* d, const Seg* segs,
+                         const unsigned long long* nsegs, int big_class, Seg* fallback,
+                         unsigned long long* fallback_count, int grid, hipStream_t st);
 void launch_local_lsd(int key_size, const SortDesc* d, const Seg* segs,
                       const unsigned long long* nsegs, int grid, hipStream_t st);
 void launch_fill(int64_t n, int kind, uint64_t seed, uint64_t first, void* keys,

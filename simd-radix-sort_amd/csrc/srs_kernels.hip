@@ -333,7 +333,7 @@ __device__ __forceinline__ int64_t xcd_remap(int64_t bid, int64_t nwg) {
 // count: per-tile digit histogram (bin-major per segment) + varying bits
 // ---------------------------------------------------------------------------
 template <typename KT, typename U, bool LUT>
-__global__ __launch_bounds__(kScatterThreads) void count_kernel(
+__global__ __launch_bounds__(kCountThreads) void count_kernel(
     const SortDesc* __restrict__ desc, const SegPlan* __restrict__ plan,
     const int32_t* __restrict__ tile_seg, uint32_t* __restrict__ hist,
     unsigned long long* __restrict__ var_or) {
@@ -352,7 +352,7 @@ __global__ __launch_bounds__(kScatterThreads) void count_kernel(
   const int32_t* lut = desc->digit_lut;
   const int lut_shift = desc->lut_shift;
 
-  for (uint32_t i = threadIdx.x; i < nb; i += kScatterThreads) h[i] = 0;
+  for (uint32_t i = threadIdx.x; i < nb; i += kCountThreads) h[i] = 0;
   if (threadIdx.x == 0) sh_or = 0;
   __syncthreads();
 
@@ -360,16 +360,16 @@ __global__ __launch_bounds__(kScatterThreads) void count_kernel(
   const int64_t rem = P.len - tl * kTile;
   const int cnt = rem < kTile ? (int)rem : kTile;
   const U uref = xf((U) * (const KT*)(kp + P.start * (int64_t)ks));
-  U raw[kScatterItems];
+  U raw[kCountItems];
 #pragma unroll
-  for (int k = 0; k < kScatterItems; k++) {
-    const int e = k * kScatterThreads + threadIdx.x;
+  for (int k = 0; k < kCountItems; k++) {
+    const int e = k * kCountThreads + threadIdx.x;
     raw[k] = e < cnt ? (U) * (const KT*)(kp + (base + e) * (int64_t)ks) : (U)0;
   }
   U vor = 0;
 #pragma unroll
-  for (int k = 0; k < kScatterItems; k++) {
-    const int e = k * kScatterThreads + threadIdx.x;
+  for (int k = 0; k < kCountItems; k++) {
+    const int e = k * kCountThreads + threadIdx.x;
     if (e < cnt) {
       const U u = xf(raw[k]);
       atomicAdd(&h[pass_digit<LUT>(u, P.shift, mask, lut, lut_shift)], 1u);
@@ -380,7 +380,7 @@ __global__ __launch_bounds__(kScatterThreads) void count_kernel(
   __syncthreads();
   // tile-major row: one coalesced 4*nb-byte write per tile
   uint32_t* row = hist + t * kMaxBins;
-  for (uint32_t i = threadIdx.x; i < nb; i += kScatterThreads) row[i] = h[i];
+  for (uint32_t i = threadIdx.x; i < nb; i += kCountThreads) row[i] = h[i];
   if (threadIdx.x == 0 && sh_or) {
     // most tiles add no new bits: skip the (contended) atomic then
     const unsigned long long known =
@@ -929,12 +929,14 @@ __device__ __forceinline__ void local_digit_pass(
   lds_barrier();
 }
 
-template <typename KT, typename U, int NT>
+// Fast path: bucket pass with LDS atomics (order inside a bucket arbitrary);
+// the rank step then restores the stable order from the packed
+// (key bits, original index) words.
+template <typename KT, typename U, int NT, int IT>
 __global__ __launch_bounds__(NT) void local_kernel(const SortDesc* __restrict__ desc,
                                                    const Seg* __restrict__ segs,
                                                    Seg* __restrict__ fallback,
                                                    unsigned long long* fallback_count) {
-  constexpr int IT = kLocalItems;
   constexpr int NW = NT / 64;
   constexpr int CAP = NT * IT;
   constexpr int IDXB = CAP <= 4096 ? 12 : 13;  // bits of an index inside the segment
@@ -942,16 +944,14 @@ __global__ __launch_bounds__(NT) void local_kernel(const SortDesc* __restrict__ 
   constexpr int NB = 1 << kLocalTopBits;
   constexpr int BPT = NB / NT;
   static_assert(BPT >= 1 && BPT * NT == NB, "bins per thread");
-  static_assert(NW * NB == CAP, "ballot counters and the permutation share storage");
   // sbuf: packed sort words during the sort, column staging afterwards
   __shared__ uint64_t sbuf[CAP];
-  __shared__ uint16_t wc_perm[CAP];       // ballot counters [NW][NB], then perm[CAP]
-  __shared__ uint32_t bflag[NB];          // bucket holds differing keys
+  __shared__ uint16_t perm[CAP];          // output slot -> original index
+  __shared__ uint32_t hist[NB];           // bucket sizes, then insertion cursors
   __shared__ uint32_t bin_start[NB + 1];
   __shared__ uint32_t scan_sh[NW + 1];
   __shared__ unsigned long long sh_or;
   __shared__ int maxlen;
-  uint16_t* perm = wc_perm;               // output slot -> original index
 
   const Seg g = segs[blockIdx.x];
   const uint32_t wave = threadIdx.x >> 6;
@@ -971,8 +971,7 @@ __global__ __launch_bounds__(NT) void local_kernel(const SortDesc* __restrict__ 
     sh_or = 0;
     maxlen = 0;
   }
-  for (uint32_t i = threadIdx.x; i < (uint32_t)CAP; i += NT) wc_perm[i] = 0;
-  for (uint32_t i = threadIdx.x; i < (uint32_t)NB; i += NT) bflag[i] = 0;
+  for (uint32_t i = threadIdx.x; i < (uint32_t)NB; i += NT) hist[i] = 0;
 
   // ---- 1. keys (column 0 holds the key in its low bytes) -------------------
   uint64_t v0[IT];
@@ -1006,6 +1005,223 @@ __global__ __launch_bounds__(NT) void local_kernel(const SortDesc* __restrict__ 
     if (hi + 1 + IDXB > 64) {
       if (threadIdx.x == 0) fallback[atomicAdd(fallback_count, 1ull)] = g;
       return;
+    }
+    const int nbits = (hi - lo + 1) < kLocalTopBits ? (hi - lo + 1) : kLocalTopBits;
+    const int sh = hi - nbits + 1;
+    const uint32_t mask = (1u << nbits) - 1;
+    const uint64_t keep = (hi == 63) ? ~0ull : ((1ull << (hi + 1)) - 1);
+    // ---- 2. bucket pass on the top varying bits (LDS atomics) -------------
+#pragma unroll
+    for (int k = 0; k < IT; k++)
+      if (valid(k)) atomicAdd(&hist[(uint32_t)(ukey(k) >> sh) & mask], 1u);
+    lds_barrier();
+    {
+      uint32_t tb[BPT], tsum = 0;
+#pragma unroll
+      for (int q = 0; q < BPT; q++) {
+        tb[q] = hist[threadIdx.x * BPT + q];
+        tsum += tb[q];
+      }
+      uint32_t tot;
+      uint32_t ex = block_excl_scan_lds<NT>(tsum, scan_sh, &tot);
+      int mymax = 0;
+#pragma unroll
+      for (int q = 0; q < BPT; q++) {
+        bin_start[threadIdx.x * BPT + q] = ex;
+        hist[threadIdx.x * BPT + q] = ex;  // becomes the insertion cursor
+        ex += tb[q];
+        mymax = (int)tb[q] > mymax ? (int)tb[q] : mymax;
+      }
+      if (threadIdx.x == 0) bin_start[NB] = tot;
+      if (mymax > 0) atomicMax(&maxlen, mymax);
+    }
+    lds_barrier();
+    STAMP();  // 2: bucket histogram
+    if (maxlen > kRankSortMax) {
+      // a large bucket (duplicates or skew): local_stable_kernel takes the
+      // segment (nothing has been written to global memory yet)
+      if (threadIdx.x == 0) fallback[atomicAdd(fallback_count, 1ull)] = g;
+      return;
+    }
+#pragma unroll
+    for (int k = 0; k < IT; k++) {
+      if (valid(k)) {
+        const U uk = ukey(k);
+        const uint32_t p = atomicAdd(&hist[(uint32_t)(uk >> sh) & mask], 1u);
+        sbuf[p] = (((uint64_t)uk & keep) << IDXB) | (uint64_t)(ebase + k * 64);
+      }
+    }
+    lds_barrier();
+    STAMP();  // 3: bucket scatter
+    // ---- 3. rank inside each bucket: #(words of the bucket below mine) ----
+    // The word orders by (key, original index), so the result is stable.
+    // Slots in two halves bound register use; a wave-uniform trip count
+    // keeps several LDS reads in flight.
+    constexpr int H = IT / 2;
+#pragma unroll
+    for (int half = 0; half < 2; half++) {
+      uint64_t x[H];
+      uint32_t bs[H], bl[H], r[H];
+      int wmax = 0;
+#pragma unroll
+      for (int i = 0; i < H; i++) {
+        const int p = (half * H + i) * NT + (int)threadIdx.x;
+        bl[i] = 0;
+        bs[i] = 0;
+        x[i] = 0;
+        r[i] = 0;
+        if (p < cnt) {
+          x[i] = sbuf[p];
+          const uint32_t d = (uint32_t)(x[i] >> (sh + IDXB)) & mask;
+          bs[i] = bin_start[d];
+          bl[i] = bin_start[d + 1] - bs[i];
+          wmax = (int)bl[i] > wmax ? (int)bl[i] : wmax;
+        }
+      }
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) {
+        const int t2 = __shfl_xor(wmax, o, 64);
+        wmax = t2 > wmax ? t2 : wmax;
+      }
+      for (int j = 0; j < wmax; j++) {
+#pragma unroll
+        for (int i = 0; i < H; i++)
+          if ((uint32_t)j < bl[i]) r[i] += sbuf[bs[i] + j] < x[i];
+      }
+#pragma unroll
+      for (int i = 0; i < H; i++) {
+        const int p = (half * H + i) * NT + (int)threadIdx.x;
+        if (p < cnt) perm[bs[i] + r[i]] = (uint16_t)(x[i] & ((1u << IDXB) - 1));
+      }
+    }
+    lds_barrier();
+    STAMP();  // 4: ranked
+  } else if (g.buf == BUF_OUT) {
+    return;  // all keys equal and already home
+  } else {
+#pragma unroll
+    for (int k = 0; k < IT; k++) perm[ebase + k * 64] = (uint16_t)(ebase + k * 64);
+    lds_barrier();
+  }
+  // output slot e takes input element perm[e]
+  uint32_t id[IT];
+#pragma unroll
+  for (int k = 0; k < IT; k++) id[k] = perm[ebase + k * 64];
+
+  // ---- 4. columns: stage in input order, write in output order --------------
+  // (in place is safe: every load of a column completes before the barrier
+  // that precedes its stores)
+  for (int c = 0; c < ncols; c++) {
+    const char* src = desc->cols[c].base[g.buf];
+    char* out = desc->cols[c].base[BUF_OUT];
+    const uint32_t w = desc->cols[c].width, st = desc->cols[c].stride;
+    uint64_t v[IT];
+    if (c == 0) {
+#pragma unroll
+      for (int k = 0; k < IT; k++) v[k] = v0[k];
+    } else {
+#pragma unroll
+      for (int k = 0; k < IT; k++) {
+        const int e = ebase + k * 64;
+        v[k] = e < cnt ? load_w(src + (base + e) * (int64_t)st, w) : 0;
+      }
+    }
+    lds_barrier();  // previous users of sbuf are done
+#pragma unroll
+    for (int k = 0; k < IT; k++)
+      if (valid(k)) sbuf[ebase + k * 64] = v[k];
+    lds_barrier();
+#pragma unroll
+    for (int k = 0; k < IT; k++) {
+      const int e = ebase + k * 64;
+      if (valid(k)) store_w(out + (base + e) * (int64_t)st, w, sbuf[id[k]]);
+    }
+    STAMP();  // 5, 6: column moved
+  }
+  STAMP_FLUSH(1);
+}
+
+// Stable path for segments the fast kernel handed over (a top-digit bucket
+// larger than kRankSortMax): the bucket pass ranks with ballots (stable), so
+// buckets whose keys are all equal are final; only mixed buckets are ranked.
+// Grid-stride over a device-side list whose length is read on device.
+template <typename KT, typename U, int NT>
+__global__ __launch_bounds__(NT) void local_stable_kernel(
+    const SortDesc* __restrict__ desc, const Seg* __restrict__ segs,
+    const unsigned long long* __restrict__ nsegs, Seg* __restrict__ fallback,
+    unsigned long long* fallback_count) {
+  constexpr int IT = kLocalStableItems;
+  constexpr int NW = NT / 64;
+  constexpr int CAP = NT * IT;
+  constexpr int IDXB = CAP <= 4096 ? 12 : 13;  // bits of an index inside the segment
+  static_assert((1 << IDXB) >= CAP, "index bits");
+  constexpr int NB = 1 << kLocalTopBits;
+  constexpr int BPT = NB / NT;
+  static_assert(BPT >= 1 && BPT * NT == NB, "bins per thread");
+  static_assert(NW * NB == CAP, "ballot counters and the permutation share storage");
+  // sbuf: packed sort words during the sort, column staging afterwards
+  __shared__ uint64_t sbuf[CAP];
+  __shared__ uint16_t wc_perm[CAP];       // ballot counters [NW][NB], then perm[CAP]
+  __shared__ uint32_t bflag[NB];          // bucket holds differing keys
+  __shared__ uint32_t bin_start[NB + 1];
+  __shared__ uint32_t scan_sh[NW + 1];
+  __shared__ unsigned long long sh_or;
+  __shared__ int maxlen;
+  uint16_t* perm = wc_perm;               // output slot -> original index
+
+  const uint32_t wave = threadIdx.x >> 6;
+  const uint32_t lane = lane_id();
+  const int ebase = (int)wave * IT * 64 + (int)lane;  // element of slot k: ebase + 64 k
+  Xform<U> xf;
+  xf.init(*desc);
+  const int ncols = desc->ncols;
+  const int kbytes = desc->key_bits >> 3;
+  const uint64_t kmask = kbytes == 8 ? ~0ull : ((1ull << (8 * kbytes)) - 1);
+  const unsigned long long total = *nsegs;
+  for (unsigned long long si = blockIdx.x; si < total; si += gridDim.x) {
+  const Seg g = segs[si];
+  const int cnt = (int)g.len;
+  const int64_t base = g.start;
+  __syncthreads();  // the previous segment is done with the shared arrays
+
+  if (threadIdx.x == 0) {
+    sh_or = 0;
+    maxlen = 0;
+  }
+  for (uint32_t i = threadIdx.x; i < (uint32_t)CAP; i += NT) wc_perm[i] = 0;
+  for (uint32_t i = threadIdx.x; i < (uint32_t)NB; i += NT) bflag[i] = 0;
+
+  // ---- 1. keys (column 0 holds the key in its low bytes) -------------------
+  uint64_t v0[IT];
+  {
+    const char* src = desc->cols[0].base[g.buf];
+    const uint32_t w = desc->cols[0].width, st = desc->cols[0].stride;
+#pragma unroll
+    for (int k = 0; k < IT; k++) {
+      const int e = ebase + k * 64;
+      v0[k] = e < cnt ? load_w(src + (base + e) * (int64_t)st, w) : 0;
+    }
+  }
+  const U uref = xf((U)(load_w(desc->cols[0].base[g.buf] + base * (int64_t)desc->cols[0].stride,
+                               desc->cols[0].width) & kmask));
+  // keys are recomputed from v0 when needed (holding them costs occupancy)
+  auto ukey = [&](int k) -> U { return xf((U)(v0[k] & kmask)); };
+  auto valid = [&](int k) -> bool { return ebase + k * 64 < cnt; };
+  U vor = 0;
+#pragma unroll
+  for (int k = 0; k < IT; k++)
+    if (valid(k)) vor |= ukey(k) ^ uref;
+  if (vor) atomicOr(&sh_or, (unsigned long long)vor);
+  lds_barrier();
+  const unsigned long long var = sh_or;
+
+  if (var != 0) {
+    const int lo = __ffsll((long long)var) - 1;
+    const int hi = 63 - __clzll((long long)var);
+    // the sort word packs (key bits 0..hi, original index): needs hi+1+IDXB <= 64
+    if (hi + 1 + IDXB > 64) {
+      if (threadIdx.x == 0) fallback[atomicAdd(fallback_count, 1ull)] = g;
+      continue;
     }
     const int nbits = (hi - lo + 1) < kLocalTopBits ? (hi - lo + 1) : kLocalTopBits;
     const int sh = hi - nbits + 1;
@@ -1049,7 +1265,6 @@ __global__ __launch_bounds__(NT) void local_kernel(const SortDesc* __restrict__ 
       }
     }
     lds_barrier();
-    STAMP();  // 2: stable bucket pass
     // ---- 3. buckets whose keys all equal are final (the pass was stable) --
 #pragma unroll
     for (int i = 0; i < IT; i++) {
@@ -1072,12 +1287,11 @@ __global__ __launch_bounds__(NT) void local_kernel(const SortDesc* __restrict__ 
       if (mymax > 0) atomicMax(&maxlen, mymax);
     }
     lds_barrier();
-    STAMP();  // 3: bucket flags
     if (maxlen > kRankSortMax) {
       // a large bucket of differing keys: local_lsd_kernel takes the segment
       // (nothing has been written to global memory yet)
       if (threadIdx.x == 0) fallback[atomicAdd(fallback_count, 1ull)] = g;
-      return;
+      continue;
     }
     // ---- 4. rank inside mixed buckets: #(words of the bucket below mine) --
     // The word orders by (key, original index): stable. Slots in two halves
@@ -1122,9 +1336,8 @@ __global__ __launch_bounds__(NT) void local_kernel(const SortDesc* __restrict__ 
       }
     }
     lds_barrier();
-    STAMP();  // 4: ranked
   } else if (g.buf == BUF_OUT) {
-    return;  // all keys equal and already home
+    continue;  // all keys equal and already home
   } else {
 #pragma unroll
     for (int k = 0; k < IT; k++) perm[ebase + k * 64] = (uint16_t)(ebase + k * 64);
@@ -1163,20 +1376,20 @@ __global__ __launch_bounds__(NT) void local_kernel(const SortDesc* __restrict__ 
       const int e = ebase + k * 64;
       if (valid(k)) store_w(out + (base + e) * (int64_t)st, w, sbuf[id[k]]);
     }
-    STAMP();  // 5, 6: column moved (loads, staging, stores drained)
   }
-  STAMP_FLUSH(1);
+  }
 }
+
 
 // Fallback for segments whose top-digit buckets are too large for the rank
 // step (skewed keys): stable LSD passes (ballot ranks) over every varying
 // bit. Grid-stride over a device-side list whose length is read on device.
 template <typename KT, typename U>
-__global__ __launch_bounds__(kLocalThreads) void local_lsd_kernel(
+__global__ __launch_bounds__(kLocalStableThreads) void local_lsd_kernel(
     const SortDesc* __restrict__ desc, const Seg* __restrict__ segs,
     const unsigned long long* __restrict__ nsegs) {
-  constexpr int NT = kLocalThreads;
-  constexpr int IT = kLocalItems;
+  constexpr int NT = kLocalStableThreads;
+  constexpr int IT = kLocalStableItems;
   constexpr int NW = NT / 64;
   constexpr int CAP = NT * IT;
   constexpr int NB = 1 << kLocalBits;
@@ -1336,10 +1549,10 @@ void launch_count(int key_size, const SortDesc* d, const SegPlan* plan,
                   unsigned long long* var_or, bool lut, hipStream_t st) {
 #define CALL(KT, U)                                                                        \
   if (lut)                                                                                 \
-    count_kernel<KT, U, true><<<(unsigned)ntiles, kScatterThreads, 0, st>>>(d, plan, tile_seg, \
+    count_kernel<KT, U, true><<<(unsigned)ntiles, kCountThreads, 0, st>>>(d, plan, tile_seg, \
                                                                           hist, var_or);   \
   else                                                                                     \
-    count_kernel<KT, U, false><<<(unsigned)ntiles, kScatterThreads, 0, st>>>(d, plan, tile_seg, \
+    count_kernel<KT, U, false><<<(unsigned)ntiles, kCountThreads, 0, st>>>(d, plan, tile_seg, \
                                                                            hist, var_or)
   SRS_KEY_DISPATCH(key_size, CALL)
 #undef CALL
@@ -1400,18 +1613,35 @@ void launch_local(int key_size, const SortDesc* d, const Seg* segs, int64_t nseg
                   Seg* fallback, unsigned long long* fallback_count, hipStream_t st) {
 #define CALL(KT, U)                                                                  \
   if (big_class)                                                                     \
-    local_kernel<KT, U, kLocalThreads>                                               \
+    local_kernel<KT, U, kLocalThreads, kLocalItems>                                  \
         <<<(unsigned)nsegs, kLocalThreads, 0, st>>>(d, segs, fallback, fallback_count); \
   else                                                                               \
-    local_kernel<KT, U, kLocalThreadsSmall>                                          \
+    local_kernel<KT, U, kLocalThreadsSmall, kLocalItemsSmall>                        \
         <<<(unsigned)nsegs, kLocalThreadsSmall, 0, st>>>(d, segs, fallback, fallback_count)
+  SRS_KEY_DISPATCH(key_size, CALL)
+#undef CALL
+}
+
+void launch_local_stable(int key_size, const SortDesc* d, const Seg* segs,
+                         const unsigned long long* nsegs, int big_class, Seg* fallback,
+                         unsigned long long* fallback_count, int grid, hipStream_t st) {
+#define CALL(KT, U)                                                                    \
+  if (big_class)                                                                       \
+    local_stable_kernel<KT, U, kLocalStableThreads>                                    \
+        <<<(unsigned)grid, kLocalStableThreads, 0, st>>>(d, segs, nsegs, fallback,      \
+                                                         fallback_count);              \
+  else                                                                                 \
+    local_stable_kernel<KT, U, kLocalStableThreads / 2>                                \
+        <<<(unsigned)grid, kLocalStableThreads / 2, 0, st>>>(d, segs, nsegs, fallback,  \
+                                                             fallback_count)
   SRS_KEY_DISPATCH(key_size, CALL)
 #undef CALL
 }
 
 void launch_local_lsd(int key_size, const SortDesc* d, const Seg* segs,
                       const unsigned long long* nsegs, int grid, hipStream_t st) {
-#define CALL(KT, U) local_lsd_kernel<KT, U><<<(unsigned)grid, kLocalThreads, 0, st>>>(d, segs, nsegs)
+#define CALL(KT, U) \
+  local_lsd_kernel<KT, U><<<(unsigned)grid, kLocalStableThreads, 0, st>>>(d, segs, nsegs)
   SRS_KEY_DISPATCH(key_size, CALL)
 #undef CALL
 }
@@ -1468,6 +1698,8 @@ __global__ void init_lists_kernel(Seg seg0, int to_local, Seg* big, Seg* local,
     ctr->n_local2 = (to_local && !small) ? 1 : 0;
     ctr->n_copy = 0;
     ctr->n_fallback = 0;
+    ctr->n_fallback1 = 0;
+    ctr->n_fallback2 = 0;
     ctr->local_elems = to_local ? (unsigned long long)seg0.len : 0;
     if (to_local) (small ? local : local2)[0] = seg0; else big[0] = seg0;
   }
