@@ -48,10 +48,36 @@ def parse():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--n", type=float, default=1e9, help="keys per GPU")
     ap.add_argument("--config", default="c1", choices=sorted(CONFIGS))
-    ap.add_argument("--cpu-sample", type=float, default=2 ** 27,
+    ap.add_argument("--cpu-sample", type=float, default=2 ** 29,
                     help="keys in the bounded CPU-baseline sample (0 = skip)")
     ap.add_argument("--no-verify", action="store_true")
     return ap.parse_args()
+
+
+def pmc_traffic(kernel, workload, n):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC
+    passes (profiles/<round>_pmc.json, written by tools/profile_summary.py
+    from FETCH_SIZE x2 + WRITE_SIZE) of this same workload, or None. PMC
+    counters cannot be read from inside the timed process, so the number is
+    the profiled run's, matched on workload and size; the latest round wins."""
+    import glob
+    best = None
+    for path in sorted(glob.glob(os.path.join(REPO, "profiles", "*_pmc.json"))):
+        try:
+            with open(path) as f:
+                doc = json.load(f)
+        except (OSError, ValueError):
+            continue
+        if doc.get("keys_per_gpu") != n or not str(doc.get("workload", "")).endswith(workload):
+            continue
+        ks = [v for v in doc.get("kernels", {}).values() if v.get("name") == kernel]
+        if not ks:
+            continue
+        tot = sum(v["hbm_bytes"] * v["dispatches"] for v in ks)
+        cnt = sum(v["dispatches"] for v in ks)
+        if cnt:
+            best = round(tot / cnt)
+    return best
 
 
 def kind_id(name):
@@ -216,7 +242,7 @@ def main():
         achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
         roofline = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1),
                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                    "traffic": None,
+                    "traffic": pmc_traffic(dom, cdesc, n) if world == 1 else None,
                     "bytes_per_launch": bytes_per_launch, "avg_launch_ms": round(avg_ms, 4)}
 
     # pass-model yardstick: B_alg = n*[L_g*(c+2s)+2s]
