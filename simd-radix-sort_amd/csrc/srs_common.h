@@ -97,6 +97,12 @@ struct ListCounters {
 #ifndef SRS_SCATTER_WG_PER_CU
 #define SRS_SCATTER_WG_PER_CU 2
 #endif
+#ifndef SRS_LOCAL_PREFETCH
+#define SRS_LOCAL_PREFETCH 0
+#endif
+#ifndef SRS_LOCAL_RANK_SPLIT
+#define SRS_LOCAL_RANK_SPLIT 2
+#endif
 #ifndef SRS_LOCAL_KEEP_KEYS
 #define SRS_LOCAL_KEEP_KEYS 0
 #endif
@@ -111,6 +117,7 @@ constexpr int kCountItems = kTile / kCountThreads;
 static_assert(kCountItems * kCountThreads == kTile, "count block shape");
 constexpr int kMaxDigitBits = 9;
 constexpr int kMaxBins = 1 << kMaxDigitBits;   // histogram row stride (tile-major)
+static_assert(kScatterThreads >= kMaxBins, "the scatter tile scan gives one bin per thread");
 constexpr int kScanGroup = 256;                 // tiles per column-scan group
 constexpr int kHistMaxBits = 12;                // srs_key_histogram_device
 
@@ -132,6 +139,9 @@ constexpr int kLocalCap = kLocalThreads * kLocalItems;    // 8192 keys per segme
 constexpr int kLocalItemsSmall = 8;
 constexpr int kLocalThreadsSmall = 512;
 constexpr int kLocalCapSmall = kLocalThreadsSmall * kLocalItemsSmall;  // 4096
+// occupancy the LDS footprint allows (90 KB -> 1 block/CU; 49 KB -> 3 blocks/CU)
+constexpr int kLocalWavesPerEU = kLocalThreads / 64 / 4;
+constexpr int kLocalWavesPerEUSmall = 3 * kLocalThreadsSmall / 64 / 4;
 constexpr int kLocalStableThreads = 512;
 constexpr int kLocalStableItems = 16;
 static_assert(kLocalStableThreads * kLocalStableItems == kLocalCap, "fallback capacity");

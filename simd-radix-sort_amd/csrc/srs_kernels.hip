@@ -37,6 +37,41 @@ __device__ __forceinline__ uint64_t load_w(const char* p, uint32_t w) {
   }
 }
 
+// Width-templated accessors. Hot loops dispatch on the (uniform) column width
+// ONCE, outside the unrolled loop (with_width), so that a tile's loads issue
+// back to back; a switch per element serialises them (measured: the scatter
+// and local kernels ran 25-30 % slower).
+template <int W>
+__device__ __forceinline__ uint64_t ldw(const char* p) {
+  if constexpr (W == 1) return *(const uint8_t*)p;
+  else if constexpr (W == 2) return *(const uint16_t*)p;
+  else if constexpr (W == 4) return *(const uint32_t*)p;
+  else return *(const uint64_t*)p;
+}
+
+template <int W>
+__device__ __forceinline__ void stw(char* p, uint64_t v) {
+  if constexpr (W == 1) *(uint8_t*)p = (uint8_t)v;
+  else if constexpr (W == 2) *(uint16_t*)p = (uint16_t)v;
+  else if constexpr (W == 4) *(uint32_t*)p = (uint32_t)v;
+  else *(uint64_t*)p = v;
+}
+
+template <int W>
+struct WidthTag {
+  static constexpr int value = W;
+};
+
+template <typename F>
+__device__ __forceinline__ void with_width(uint32_t w, F&& f) {
+  switch (w) {
+    case 1: f(WidthTag<1>{}); break;
+    case 2: f(WidthTag<2>{}); break;
+    case 4: f(WidthTag<4>{}); break;
+    default: f(WidthTag<8>{}); break;
+  }
+}
+
 __device__ __forceinline__ void store_w(char* p, uint32_t w, uint64_t v) {
   switch (w) {
     case 1: *(uint8_t*)p = (uint8_t)v; break;
@@ -648,6 +683,12 @@ __global__ __launch_bounds__(kMaxBins) void tile_offs_kernel(
 // store would wait for it). HBM then always has a tile's worth of loads in
 // flight per workgroup, and neighbouring tiles' runs into one bucket are
 // written by one workgroup (their partial lines meet in one L2).
+#define SCATTER_STORE stw
+#if SRS_DEBUG_SEQ_WRITE  // timing experiment only: every tile written in place, unsorted order
+#define SCATTER_DST(d) (ti.base)
+#else
+#define SCATTER_DST(d) (L.gdst[d])
+#endif
 struct ScatterLds {
   uint64_t sval[kTile];
   uint16_t wc[kScatterThreads / 64][kMaxBins];
@@ -679,20 +720,24 @@ __device__ __forceinline__ TileInfo scatter_load_tile(
   {
     const char* src = desc->cols[0].base[P.buf];
     const uint32_t w = desc->cols[0].width, st = desc->cols[0].stride;
+with_width(w, [&](auto W_) {
 #pragma unroll
-    for (int k = 0; k < IT; k++) {
-      const int e = ebase + k * 64;
-      v0[k] = e < ti.cnt ? load_w(src + (ti.base + e) * (int64_t)st, w) : 0;
-    }
+  for (int k = 0; k < IT; k++) {
+    const int e = ebase + k * 64;
+    v0[k] = e < ti.cnt ? ldw<decltype(W_)::value>(src + (ti.base + e) * (int64_t)st) : 0;
+  }
+});
   }
   if (ncols > 1) {
     const char* src = desc->cols[1].base[P.buf];
     const uint32_t w = desc->cols[1].width, st = desc->cols[1].stride;
+with_width(w, [&](auto W_) {
 #pragma unroll
-    for (int k = 0; k < IT; k++) {
-      const int e = ebase + k * 64;
-      v1[k] = e < ti.cnt ? load_w(src + (ti.base + e) * (int64_t)st, w) : 0;
-    }
+  for (int k = 0; k < IT; k++) {
+    const int e = ebase + k * 64;
+    v1[k] = e < ti.cnt ? ldw<decltype(W_)::value>(src + (ti.base + e) * (int64_t)st) : 0;
+  }
+});
   }
   my_off = 0;
   if (ti.cnt > 0 && threadIdx.x < (1u << P.bits)) my_off = (int64_t)offs[t * kMaxBins + threadIdx.x];
@@ -773,27 +818,31 @@ __device__ __forceinline__ void scatter_process_tile(
   {
     char* out = desc->cols[0].base[P.dst];
     const uint32_t w = desc->cols[0].width, st = desc->cols[0].stride;
+    with_width(w, [&](auto W_) {
 #pragma unroll
-    for (int i = 0; i < IT; i++) {
-      const int j = i * NT + (int)threadIdx.x;
-      dout[i] = 0;
-      if (j < cnt) {
-        const uint64_t x = L.sval[j];
-        const uint32_t d = pass_digit<LUT>(xf((U)(x & kmask)), P.shift, mask, lut, lut_shift);
-        dout[i] = (uint16_t)d;
-        store_w(out + ((int64_t)j + L.gdst[d]) * (int64_t)st, w, x);
+      for (int i = 0; i < IT; i++) {
+        const int j = i * NT + (int)threadIdx.x;
+        dout[i] = 0;
+        if (j < cnt) {
+          const uint64_t x = L.sval[j];
+          const uint32_t d = pass_digit<LUT>(xf((U)(x & kmask)), P.shift, mask, lut, lut_shift);
+          dout[i] = (uint16_t)d;
+          SCATTER_STORE<decltype(W_)::value>(out + ((int64_t)j + SCATTER_DST(d)) * (int64_t)st, x);
+        }
       }
-    }
+    });
   }
   for (int c = 1; c < ncols; c++) {
     const uint32_t cw = desc->cols[c].width, cst = desc->cols[c].stride;
     if (c > 1) {
       const char* src = desc->cols[c].base[P.buf];
+with_width(cw, [&](auto W_) {
 #pragma unroll
-      for (int k = 0; k < IT; k++) {
-        const int e = ebase + k * 64;
-        v1[k] = e < cnt ? load_w(src + (ti.base + e) * (int64_t)cst, cw) : 0;
-      }
+  for (int k = 0; k < IT; k++) {
+    const int e = ebase + k * 64;
+    v1[k] = e < cnt ? ldw<decltype(W_)::value>(src + (ti.base + e) * (int64_t)cst) : 0;
+  }
+});
     }
     lds_barrier();  // every slot of the previous column has been read
 #pragma unroll
@@ -801,11 +850,15 @@ __device__ __forceinline__ void scatter_process_tile(
       if (valid(k)) L.sval[pos[k]] = v1[k];
     lds_barrier();
     char* out = desc->cols[c].base[P.dst];
+    with_width(cw, [&](auto W_) {
 #pragma unroll
-    for (int i = 0; i < IT; i++) {
-      const int j = i * NT + (int)threadIdx.x;
-      if (j < cnt) store_w(out + ((int64_t)j + L.gdst[dout[i]]) * (int64_t)cst, cw, L.sval[j]);
-    }
+      for (int i = 0; i < IT; i++) {
+        const int j = i * NT + (int)threadIdx.x;
+        if (j < cnt)
+          SCATTER_STORE<decltype(W_)::value>(
+              out + ((int64_t)j + SCATTER_DST(dout[i])) * (int64_t)cst, L.sval[j]);
+      }
+    });
   }
   STAMP();  // 5: all stores issued (and, in stamp builds, drained)
   STAMP_FLUSH(0);
@@ -932,8 +985,8 @@ __device__ __forceinline__ void local_digit_pass(
 // Fast path: bucket pass with LDS atomics (order inside a bucket arbitrary);
 // the rank step then restores the stable order from the packed
 // (key bits, original index) words.
-template <typename KT, typename U, int NT, int IT>
-__global__ __launch_bounds__(NT) void local_kernel(const SortDesc* __restrict__ desc,
+template <typename KT, typename U, int NT, int IT, int WPE>
+__global__ __launch_bounds__(NT, WPE) void local_kernel(const SortDesc* __restrict__ desc,
                                                    const Seg* __restrict__ segs,
                                                    Seg* __restrict__ fallback,
                                                    unsigned long long* fallback_count) {
@@ -978,12 +1031,30 @@ __global__ __launch_bounds__(NT) void local_kernel(const SortDesc* __restrict__ 
   {
     const char* src = desc->cols[0].base[g.buf];
     const uint32_t w = desc->cols[0].width, st = desc->cols[0].stride;
+with_width(w, [&](auto W_) {
 #pragma unroll
-    for (int k = 0; k < IT; k++) {
-      const int e = ebase + k * 64;
-      v0[k] = e < cnt ? load_w(src + (base + e) * (int64_t)st, w) : 0;
-    }
+  for (int k = 0; k < IT; k++) {
+    const int e = ebase + k * 64;
+    v0[k] = e < cnt ? ldw<decltype(W_)::value>(src + (base + e) * (int64_t)st) : 0;
   }
+});
+  }
+#if SRS_LOCAL_PREFETCH
+  // the first payload column is loaded with the keys: its latency then
+  // overlaps the sort instead of following it
+  uint64_t v1[IT];
+  if (ncols > 1) {
+    const char* src = desc->cols[1].base[g.buf];
+    const uint32_t w = desc->cols[1].width, st = desc->cols[1].stride;
+with_width(w, [&](auto W_) {
+#pragma unroll
+  for (int k = 0; k < IT; k++) {
+    const int e = ebase + k * 64;
+    v1[k] = e < cnt ? ldw<decltype(W_)::value>(src + (base + e) * (int64_t)st) : 0;
+  }
+});
+  }
+#endif
   const U uref = xf((U)(load_w(desc->cols[0].base[g.buf] + base * (int64_t)desc->cols[0].stride,
                                desc->cols[0].width) & kmask));
   // keys are recomputed from v0 when needed (holding them costs occupancy)
@@ -1057,9 +1128,10 @@ __global__ __launch_bounds__(NT) void local_kernel(const SortDesc* __restrict__ 
     // The word orders by (key, original index), so the result is stable.
     // Slots in two halves bound register use; a wave-uniform trip count
     // keeps several LDS reads in flight.
-    constexpr int H = IT / 2;
+    constexpr int NH = SRS_LOCAL_RANK_SPLIT;
+    constexpr int H = IT / NH;
 #pragma unroll
-    for (int half = 0; half < 2; half++) {
+    for (int half = 0; half < NH; half++) {
       uint64_t x[H];
       uint32_t bs[H], bl[H], r[H];
       int wmax = 0;
@@ -1119,23 +1191,32 @@ __global__ __launch_bounds__(NT) void local_kernel(const SortDesc* __restrict__ 
     if (c == 0) {
 #pragma unroll
       for (int k = 0; k < IT; k++) v[k] = v0[k];
-    } else {
+#if SRS_LOCAL_PREFETCH
+    } else if (c == 1) {
 #pragma unroll
-      for (int k = 0; k < IT; k++) {
-        const int e = ebase + k * 64;
-        v[k] = e < cnt ? load_w(src + (base + e) * (int64_t)st, w) : 0;
-      }
+      for (int k = 0; k < IT; k++) v[k] = v1[k];
+#endif
+    } else {
+with_width(w, [&](auto W_) {
+#pragma unroll
+  for (int k = 0; k < IT; k++) {
+    const int e = ebase + k * 64;
+    v[k] = e < cnt ? ldw<decltype(W_)::value>(src + (base + e) * (int64_t)st) : 0;
+  }
+});
     }
     lds_barrier();  // previous users of sbuf are done
 #pragma unroll
     for (int k = 0; k < IT; k++)
       if (valid(k)) sbuf[ebase + k * 64] = v[k];
     lds_barrier();
+with_width(w, [&](auto W_) {
 #pragma unroll
-    for (int k = 0; k < IT; k++) {
-      const int e = ebase + k * 64;
-      if (valid(k)) store_w(out + (base + e) * (int64_t)st, w, sbuf[id[k]]);
-    }
+  for (int k = 0; k < IT; k++) {
+    const int e = ebase + k * 64;
+    if (valid(k)) stw<decltype(W_)::value>(out + (base + e) * (int64_t)st, sbuf[id[k]]);
+  }
+});
     STAMP();  // 5, 6: column moved
   }
   STAMP_FLUSH(1);
@@ -1196,11 +1277,13 @@ __global__ __launch_bounds__(NT) void local_stable_kernel(
   {
     const char* src = desc->cols[0].base[g.buf];
     const uint32_t w = desc->cols[0].width, st = desc->cols[0].stride;
+with_width(w, [&](auto W_) {
 #pragma unroll
-    for (int k = 0; k < IT; k++) {
-      const int e = ebase + k * 64;
-      v0[k] = e < cnt ? load_w(src + (base + e) * (int64_t)st, w) : 0;
-    }
+  for (int k = 0; k < IT; k++) {
+    const int e = ebase + k * 64;
+    v0[k] = e < cnt ? ldw<decltype(W_)::value>(src + (base + e) * (int64_t)st) : 0;
+  }
+});
   }
   const U uref = xf((U)(load_w(desc->cols[0].base[g.buf] + base * (int64_t)desc->cols[0].stride,
                                desc->cols[0].width) & kmask));
@@ -1360,22 +1443,26 @@ __global__ __launch_bounds__(NT) void local_stable_kernel(
 #pragma unroll
       for (int k = 0; k < IT; k++) v[k] = v0[k];
     } else {
+with_width(w, [&](auto W_) {
 #pragma unroll
-      for (int k = 0; k < IT; k++) {
-        const int e = ebase + k * 64;
-        v[k] = e < cnt ? load_w(src + (base + e) * (int64_t)st, w) : 0;
-      }
+  for (int k = 0; k < IT; k++) {
+    const int e = ebase + k * 64;
+    v[k] = e < cnt ? ldw<decltype(W_)::value>(src + (base + e) * (int64_t)st) : 0;
+  }
+});
     }
     lds_barrier();  // previous users of sbuf are done
 #pragma unroll
     for (int k = 0; k < IT; k++)
       if (valid(k)) sbuf[ebase + k * 64] = v[k];
     lds_barrier();
+with_width(w, [&](auto W_) {
 #pragma unroll
-    for (int k = 0; k < IT; k++) {
-      const int e = ebase + k * 64;
-      if (valid(k)) store_w(out + (base + e) * (int64_t)st, w, sbuf[id[k]]);
-    }
+  for (int k = 0; k < IT; k++) {
+    const int e = ebase + k * 64;
+    if (valid(k)) stw<decltype(W_)::value>(out + (base + e) * (int64_t)st, sbuf[id[k]]);
+  }
+});
   }
   }
 }
@@ -1420,13 +1507,16 @@ __global__ __launch_bounds__(kLocalStableThreads) void local_lsd_kernel(
     {
       const char* src = desc->cols[0].base[g.buf];
       const uint32_t w = desc->cols[0].width, st = desc->cols[0].stride;
+      with_width(w, [&](auto W_) {
 #pragma unroll
-      for (int k = 0; k < IT; k++) {
-        const int e = ebase + k * 64;
-        valid[k] = e < cnt;
-        id[k] = (uint32_t)e;
-        u[k] = valid[k] ? xf((U)(load_w(src + (base + e) * (int64_t)st, w) & kmask)) : (U)0;
-      }
+        for (int k = 0; k < IT; k++) {
+          const int e = ebase + k * 64;
+          valid[k] = e < cnt;
+          id[k] = (uint32_t)e;
+          u[k] = valid[k] ? xf((U)(ldw<decltype(W_)::value>(src + (base + e) * (int64_t)st) & kmask))
+                          : (U)0;
+        }
+      });
     }
     __syncthreads();
     const U uref = xf((U)(load_w(desc->cols[0].base[g.buf] + base * (int64_t)desc->cols[0].stride,
@@ -1461,15 +1551,19 @@ __global__ __launch_bounds__(kLocalStableThreads) void local_lsd_kernel(
       char* out = desc->cols[c].base[BUF_OUT];
       const uint32_t w = desc->cols[c].width, st = desc->cols[c].stride;
       uint64_t v[IT];
+      with_width(w, [&](auto W_) {
 #pragma unroll
-      for (int k = 0; k < IT; k++)
-        v[k] = valid[k] ? load_w(src + (base + (int64_t)id[k]) * st, w) : 0;
+        for (int k = 0; k < IT; k++)
+          v[k] = valid[k] ? ldw<decltype(W_)::value>(src + (base + (int64_t)id[k]) * st) : 0;
+      });
       __syncthreads();
+      with_width(w, [&](auto W_) {
 #pragma unroll
-      for (int k = 0; k < IT; k++) {
-        const int e = ebase + k * 64;
-        if (valid[k]) store_w(out + (base + e) * (int64_t)st, w, v[k]);
-      }
+        for (int k = 0; k < IT; k++) {
+          const int e = ebase + k * 64;
+          if (valid[k]) stw<decltype(W_)::value>(out + (base + e) * (int64_t)st, v[k]);
+        }
+      });
     }
   }
 }
@@ -1613,10 +1707,10 @@ void launch_local(int key_size, const SortDesc* d, const Seg* segs, int64_t nseg
                   Seg* fallback, unsigned long long* fallback_count, hipStream_t st) {
 #define CALL(KT, U)                                                                  \
   if (big_class)                                                                     \
-    local_kernel<KT, U, kLocalThreads, kLocalItems>                                  \
+    local_kernel<KT, U, kLocalThreads, kLocalItems, kLocalWavesPerEU>                \
         <<<(unsigned)nsegs, kLocalThreads, 0, st>>>(d, segs, fallback, fallback_count); \
   else                                                                               \
-    local_kernel<KT, U, kLocalThreadsSmall, kLocalItemsSmall>                        \
+    local_kernel<KT, U, kLocalThreadsSmall, kLocalItemsSmall, kLocalWavesPerEUSmall> \
         <<<(unsigned)nsegs, kLocalThreadsSmall, 0, st>>>(d, segs, fallback, fallback_count)
   SRS_KEY_DISPATCH(key_size, CALL)
 #undef CALL

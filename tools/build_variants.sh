@@ -5,12 +5,14 @@ set -e
 cd "$(dirname "$0")/../simd-radix-sort_amd"
 for spec in "$@"; do
   name=${spec%%:*}; flags=${spec#*:}
-  out=lib/variants/$name; mkdir -p $out build/v_$name
+  out=lib/variants/$name; rm -rf $out build/v_$name; mkdir -p $out build/v_$name
+  pids=()
   for f in srs_kernels srs_api; do
     /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -munsafe-fp-atomics $flags \
       -c csrc/$f.hip -o build/v_$name/$f.o &
+    pids+=($!)
   done
-  wait
+  for p in "${pids[@]}"; do wait $p || { echo "FAILED $name"; exit 1; }; done
   /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o $out/libsrs_amd.so build/v_$name/*.o -Wl,-rpath,/opt/rocm/lib
   echo "built $name ($flags)"
 done
