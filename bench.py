@@ -51,6 +51,8 @@ def parse():
     ap.add_argument("--cpu-sample", type=float, default=2 ** 29,
                     help="keys in the bounded CPU-baseline sample (0 = skip)")
     ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--shard", action="store_true",
+                    help="run the multi-GPU shard protocol even at one rank (RCCL, world 1)")
     return ap.parse_args()
 
 
@@ -157,7 +159,12 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    shard = world > 1 or args.shard
+    if shard:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
         torch.cuda.set_device(local_rank)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
     dev = torch.device("cuda", local_rank)
@@ -183,7 +190,7 @@ def main():
         rec_bytes = keys.element_size() + sum(psizes)
     torch.cuda.synchronize()
 
-    if world > 1:
+    if shard:
         if layout != "soa":
             raise SystemExit("multi-GPU bench runs the SoA configs (c1, c2)")
         from srs_amd.dist import HipShardOps, ShardSorter  # multi-GPU path (RCCL)
@@ -191,7 +198,7 @@ def main():
     shard_out = []
 
     def step():
-        if world > 1:
+        if shard:
             shard_out[:] = [sorter.sort(keys, pays)]
             return
         if layout == "aos":
@@ -204,19 +211,19 @@ def main():
     torch.cuda.synchronize()
     srs_amd.reset_kernel_stats()
     srs_amd.set_kernel_timing(True)
-    if world > 1:
+    if shard:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
     torch.cuda.synchronize()
-    if world > 1:
+    if shard:
         dist.barrier()
     t1 = time.perf_counter()
     srs_amd.set_kernel_timing(False)
     elapsed = t1 - t0
-    if world > 1:
+    if shard:
         tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
@@ -254,11 +261,11 @@ def main():
     pass_model_gbs = b_alg * world / (elapsed / args.steps) / 1e9
 
     verified = None
-    if not args.no_verify and world == 1:
+    if not args.no_verify and not shard:
         verified = verify(keys_out if layout == "soa" else None, pays_out if layout == "soa" else None,
-                          rec_out, kname, torch)
+                          rec_out, kname, psizes, torch)
     elif not args.no_verify:
-        verified = verify_shards(keys, pays, shard_out[0], kname, torch, dist, dev)
+        verified = verify_shards(keys, pays, shard_out[0], kname, psizes, torch, dist, dev)
 
     cpu = None
     if rank == 0 and args.cpu_sample > 0 and (world == 1):
@@ -294,7 +301,7 @@ def main():
             "verified": verified,
         }
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if shard:
         dist.destroy_process_group()
 
 
@@ -306,43 +313,86 @@ def _order_view(k, kname, torch):
     return k
 
 
-def _hash_pairs(k, p, torch):
-    """Order-independent checksum of (key, payload) pairs: sum of a mixed
-    64-bit hash (wrapping int64 arithmetic)."""
-    kk = k.view(torch.int64) if k.element_size() == 8 else k.view(torch.int32).to(torch.int64)
-    pp = p.view(torch.int64) if p.element_size() == 8 else p.view(torch.int32).to(torch.int64)
-    x = kk * 0x9E3779B97F4A7C15 + pp
-    x = x ^ ((x >> 29) & 0x7FFFFFFFF)
-    x = x * 0xBF58476D1CE4E5B9
-    return int(x.sum().item())
+def _u64_bits(x, torch):
+    """int64 view of key/payload bits (zero-extended for 4-byte types)."""
+    if x.element_size() == 8:
+        return x.view(torch.int64)
+    return x.view(torch.int32).to(torch.int64) & 0xFFFFFFFF
 
 
-def verify_shards(keys_in, pays_in, out, kname, torch, dist, dev):
-    """Multi-GPU: each rank sorted; last key of rank r <= first of rank r+1;
-    the multiset of (key, payload) pairs over all ranks is unchanged."""
+def _splitmix64(x, torch):
+    """splitmix64 in wrapping int64 arithmetic (logical shifts by masking);
+    the device generator's payload rule (srs_kernels.hip fill_kernel)."""
+    x = x + (0x9E3779B97F4A7C15 - (1 << 64))
+    x = (x ^ ((x >> 30) & ((1 << 34) - 1))) * (0xBF58476D1CE4E5B9 - (1 << 64))
+    x = (x ^ ((x >> 27) & ((1 << 37) - 1))) * (0x94D049BB133111EB - (1 << 64))
+    return x ^ ((x >> 31) & ((1 << 33) - 1))
+
+
+def _check_payloads(k, pays, psizes, torch, chunk=1 << 26):
+    """payload column c == splitmix64(bits(key) ^ c*0xD1B54A32D192ED03),
+    truncated to its width, for every element (the generator's rule)."""
+    for c, (p, w) in enumerate(zip(pays, psizes)):
+        salt = (c * 0xD1B54A32D192ED03) & ((1 << 64) - 1)
+        salt = salt - (1 << 64) if salt >= 1 << 63 else salt
+        for i in range(0, k.numel(), chunk):
+            kb = _u64_bits(k[i:i + chunk], torch)
+            f = _splitmix64(kb ^ salt, torch)
+            if w == 4:
+                f = f & 0xFFFFFFFF
+            if not bool((f == _u64_bits(p[i:i + chunk], torch)).all().item()):
+                return False
+    return True
+
+
+def _hash_pairs(k, pays, torch, chunk=1 << 26):
+    """Order-independent checksum of the records: wrapping int64 sum of a
+    mixed hash of (key, payload...)."""
+    tot = 0
+    for i in range(0, k.numel(), chunk):
+        x = _u64_bits(k[i:i + chunk], torch) * (0x9E3779B97F4A7C15 - (1 << 64))
+        for p in pays:
+            x = (x ^ _u64_bits(p[i:i + chunk], torch)) * (0xBF58476D1CE4E5B9 - (1 << 64))
+        x = x ^ ((x >> 29) & 0x7FFFFFFFF)
+        tot = (tot + int(x.sum().item())) & ((1 << 64) - 1)
+    return tot - (1 << 64) if tot >= 1 << 63 else tot
+
+
+def verify_shards(keys_in, pays_in, out, kname, psizes, torch, dist, dev):
+    """Multi-GPU: each rank sorted; last key of rank r <= first of rank r+1
+    (exact, in the transformed order); payload == f(key) everywhere; the
+    record multiset over all ranks is unchanged."""
     k, ps = out
     s = _order_view(k, kname, torch)
     ok = bool((s[1:] >= s[:-1]).all().item()) if s.numel() > 1 else True
-    ends = torch.tensor([float(s[0].item()) if s.numel() else float("inf"),
-                         float(s[-1].item()) if s.numel() else float("-inf")],
-                        dtype=torch.float64, device=dev)
+    ok = ok and _check_payloads(k, ps, psizes, torch)
     world = dist.get_world_size()
+    if s.numel():
+        ends = torch.stack([s[0], s[-1]]).to(torch.float64 if s.is_floating_point() else torch.int64)
+    else:
+        ends = torch.zeros(2, dtype=torch.float64 if s.is_floating_point() else torch.int64, device=dev)
+    cnt = torch.tensor([s.numel()], dtype=torch.int64, device=dev)
     allends = [torch.zeros_like(ends) for _ in range(world)]
+    allcnt = [torch.zeros_like(cnt) for _ in range(world)]
     dist.all_gather(allends, ends)
-    nonempty = [e.tolist() for e in allends if e[0].item() != float("inf")]
+    dist.all_gather(allcnt, cnt)
+    nonempty = [e.tolist() for e, c in zip(allends, allcnt) if c.item() > 0]
     bounds_ok = all(a[1] <= b[0] for a, b in zip(nonempty, nonempty[1:]))
-    h = torch.tensor([_hash_pairs(keys_in, pays_in[0], torch), _hash_pairs(k, ps[0], torch),
+    h = torch.tensor([_hash_pairs(keys_in, pays_in, torch), _hash_pairs(k, ps, torch),
                       keys_in.numel(), k.numel()], dtype=torch.int64, device=dev)
     dist.all_reduce(h)
     okt = torch.tensor([1 if ok else 0], device=dev)
     dist.all_reduce(okt, op=dist.ReduceOp.MIN)
-    return {"sorted": bool(okt.item()), "rank_bounds_ordered": bounds_ok,
-            "multiset_hash_equal": h[0].item() == h[1].item(), "count_equal": h[2].item() == h[3].item()}
+    return {"sorted_and_payload_eq_f_key": bool(okt.item()), "rank_bounds_ordered": bounds_ok,
+            "multiset_hash_equal": h[0].item() == h[1].item(),
+            "count_equal": h[2].item() == h[3].item()}
 
 
-def verify(keys_out, pays_out, rec_out, kname, torch):
+def verify(keys_out, pays_out, rec_out, kname, psizes, torch):
     """Size-independent checks on the full output: sortedness (transformed
-    order) and payload == f(key) for every element; plus count preserved."""
+    order) and payload == f(key) for every element. With payload = f(key)
+    the sorted output is unique, so this is bit-exact parity at full size
+    (together with the element count, fixed by construction)."""
     if rec_out is not None:
         k = rec_out[:, 0]
         p = [rec_out[:, 1]]
@@ -350,7 +400,7 @@ def verify(keys_out, pays_out, rec_out, kname, torch):
         k, p = keys_out, pays_out
     s = _order_view(k, kname, torch)
     ok = bool((s[1:] >= s[:-1]).all().item())
-    return {"sorted": ok}
+    return {"sorted": ok, "payload_eq_f_key": _check_payloads(k, p, psizes, torch)}
 
 
 if __name__ == "__main__":

@@ -879,27 +879,33 @@ __global__ __launch_bounds__(kScatterThreads, SRS_SCATTER_WAVES_PER_EU) void sca
   scatter_process_tile<KT, U, LUT>(desc, plan, L, ti, ncols, v0, v1, my_off);
 }
 
-// Persistent, software-pipelined: workgroup b owns tiles [b*chunk, (b+1)*chunk).
+// Persistent, software-pipelined: in round i the grid covers tiles
+// [i*G, (i+1)*G), XCD-aware inside the round (so that, as in the one-shot
+// kernel, tiles running at the same time are neighbours and their partial
+// bucket lines meet in one L2); a workgroup issues its next tile's loads
+// before ranking and storing the current one.
 template <typename KT, typename U, bool LUT>
 __global__ __launch_bounds__(kScatterThreads, SRS_SCATTER_WAVES_PER_EU) void scatter_pipe_kernel(
     const SortDesc* __restrict__ desc, const SegPlan* __restrict__ plan,
-    const int32_t* __restrict__ tile_seg, const uint64_t* __restrict__ offs, int64_t ntiles,
-    int64_t chunk) {
+    const int32_t* __restrict__ tile_seg, const uint64_t* __restrict__ offs, int64_t ntiles) {
   __shared__ ScatterLds L;
-  const int64_t t0 = (int64_t)blockIdx.x * chunk;
-  const int64_t t1 = min(t0 + chunk, ntiles);
-  if (t0 >= t1) return;
+  const int64_t G = gridDim.x;
+  const int64_t r = xcd_remap(blockIdx.x, G);
+  if (r >= ntiles) return;
   const int ncols = desc->ncols;
   uint64_t a0[kScatterItems], a1[kScatterItems], b0[kScatterItems], b1[kScatterItems];
   int64_t aoff, boff;
-  TileInfo ta = scatter_load_tile<KT, U>(desc, plan, tile_seg, offs, t0, ncols, a0, a1, aoff);
-  for (int64_t t = t0; t < t1; t += 2) {
+  TileInfo ta = scatter_load_tile<KT, U>(desc, plan, tile_seg, offs, r, ncols, a0, a1, aoff);
+  for (int64_t t = r; t < ntiles; t += 2 * G) {
     TileInfo tb;
     tb.cnt = 0;
-    if (t + 1 < t1) tb = scatter_load_tile<KT, U>(desc, plan, tile_seg, offs, t + 1, ncols, b0, b1, boff);
+    if (t + G < ntiles)
+      tb = scatter_load_tile<KT, U>(desc, plan, tile_seg, offs, t + G, ncols, b0, b1, boff);
     if (ta.cnt > 0) scatter_process_tile<KT, U, LUT>(desc, plan, L, ta, ncols, a0, a1, aoff);
-    if (t + 1 >= t1) break;
-    if (t + 2 < t1) ta = scatter_load_tile<KT, U>(desc, plan, tile_seg, offs, t + 2, ncols, a0, a1, aoff);
+    if (t + G >= ntiles) break;
+    ta.cnt = 0;
+    if (t + 2 * G < ntiles)
+      ta = scatter_load_tile<KT, U>(desc, plan, tile_seg, offs, t + 2 * G, ncols, a0, a1, aoff);
     if (tb.cnt > 0) scatter_process_tile<KT, U, LUT>(desc, plan, L, tb, ncols, b0, b1, boff);
   }
 }
@@ -1680,16 +1686,14 @@ void launch_scatter(int key_size, const SortDesc* d, const SegPlan* plan,
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) == hipSuccess)
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  const int64_t nwg = std::min<int64_t>(ntiles, (int64_t)cus * SRS_SCATTER_WG_PER_CU);
-  const int64_t chunk = (ntiles + nwg - 1) / nwg;
-  const int64_t grid = (ntiles + chunk - 1) / chunk;
+  const int64_t grid = std::min<int64_t>(ntiles, (int64_t)cus * SRS_SCATTER_WG_PER_CU);
 #define CALL(KT, U)                                                                        \
   if (lut)                                                                                 \
     scatter_pipe_kernel<KT, U, true><<<(unsigned)grid, kScatterThreads, 0, st>>>(          \
-        d, plan, tile_seg, offs, ntiles, chunk);                                           \
+        d, plan, tile_seg, offs, ntiles);                                                  \
   else                                                                                     \
     scatter_pipe_kernel<KT, U, false><<<(unsigned)grid, kScatterThreads, 0, st>>>(         \
-        d, plan, tile_seg, offs, ntiles, chunk)
+        d, plan, tile_seg, offs, ntiles)
 #else
 #define CALL(KT, U)                                                                         \
   if (lut)                                                                                  \

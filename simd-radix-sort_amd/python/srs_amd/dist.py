@@ -7,7 +7,10 @@ Protocol, per rank r holding n_r keys (+ payload columns):
   3. bucket -> rank map: contiguous bucket ranges with ~equal key counts
   4. stable partition of the local columns by destination rank
                                                          (srs_partition_device)
-  5. all-to-all of the group sizes, then of every column (RCCL, over xGMI)
+  5. all-gather of the group sizes, then every column moves peer to peer
+     (batched isend/irecv = RCCL's grouped send/recv over xGMI), in rounds
+     of at most 256 MB per message: RCCL corrupted a single 8 GB message
+     (measured: all_to_all_single of 1e9 int64 at world 1; 1e8 was exact)
   6. local sort of what was received                     (srs_sort_soa_device)
 Rank r then holds the r-th contiguous slice of the globally sorted array:
 every key on rank r orders before every key on rank r+1.
@@ -73,7 +76,7 @@ class ShardSorter:
     group. Buffers are allocated once (capacity = slack * n per rank)."""
 
     def __init__(self, ops, n_local: int, payload_dtypes, key_dtype, device, bits: int = 12,
-                 slack: float = 1.25, group=None):
+                 slack: float = 1.25, group=None, chunk_bytes: int = 256 << 20):
         self.ops = ops
         self.bits = bits
         self.group = group
@@ -87,6 +90,7 @@ class ShardSorter:
         self.recv_keys = torch.empty(cap, dtype=key_dtype, device=device)
         self.recv_pays = [torch.empty(cap, dtype=dt, device=device) for dt in payload_dtypes]
         self.last_counts = None
+        self.chunk_bytes = chunk_bytes
 
     def _ensure_capacity(self, total):
         if total <= self.recv_keys.numel():
@@ -95,6 +99,41 @@ class ShardSorter:
         self.recv_keys = torch.empty(cap, dtype=self.recv_keys.dtype, device=self.device)
         self.recv_pays = [torch.empty(cap, dtype=p.dtype, device=self.device)
                           for p in self.recv_pays]
+
+    def _exchange(self, send, recv, in_splits, out_splits, biggest):
+        """send: groups by destination rank; recv: groups by source rank.
+        The own group is a local copy; the others move in rounds of at most
+        `chunk_bytes` per message, every rank running the same rounds."""
+        w, me = self.world, self.rank
+        soff = [0] * w
+        roff = [0] * w
+        for i in range(1, w):
+            soff[i] = soff[i - 1] + in_splits[i - 1]
+            roff[i] = roff[i - 1] + out_splits[i - 1]
+        if in_splits[me]:
+            recv[roff[me]:roff[me] + in_splits[me]].copy_(send[soff[me]:soff[me] + in_splits[me]])
+        if w == 1:
+            return
+        C = max(1, self.chunk_bytes // send.element_size())
+        rounds = (biggest + C - 1) // C
+        s_c, r_c = _comm(send), _comm(recv)
+        for r in range(rounds):
+            a = r * C
+            ops = []
+            for peer in range(w):
+                if peer == me:
+                    continue
+                ls = min(C, in_splits[peer] - a)
+                if ls > 0:
+                    ops.append(dist.P2POp(dist.isend, s_c[soff[peer] + a:soff[peer] + a + ls], peer,
+                                          group=self.group))
+                lr = min(C, out_splits[peer] - a)
+                if lr > 0:
+                    ops.append(dist.P2POp(dist.irecv, r_c[roff[peer] + a:roff[peer] + a + lr], peer,
+                                          group=self.group))
+            if ops:
+                for req in dist.batch_isend_irecv(ops):
+                    req.wait()
 
     def sort(self, keys, pays):
         """Returns (keys, payloads) views: this rank's slice of the sorted union."""
@@ -110,22 +149,22 @@ class ShardSorter:
         # 4: stable partition by destination rank
         counts = self.ops.partition(keys, pays, self.bits, part_of_bucket, w,
                                     (self.part_keys, *self.part_pays))
-        # 5: exchange sizes, then columns
+        # 5: exchange sizes (full matrix, so every rank agrees on the rounds)
         send = torch.tensor(counts, dtype=torch.int64, device=hist.device)
-        recv = torch.empty_like(send)
-        dist.all_to_all_single(recv, send, group=self.group)
+        mat = [torch.empty_like(send) for _ in range(w)]
+        dist.all_gather(mat, send, group=self.group)
+        mat = [m.tolist() for m in mat]           # mat[src][dst]
         in_splits = [int(c) for c in counts]
-        out_splits = [int(c) for c in recv.tolist()]
+        out_splits = [int(mat[src][self.rank]) for src in range(w)]
         total = sum(out_splits)
         self._ensure_capacity(total)
+        biggest = max(max(row) for row in mat)
         rk = self.recv_keys[:total]
-        dist.all_to_all_single(_comm(rk), _comm(self.part_keys[:keys.numel()]), out_splits,
-                               in_splits, group=self.group)
+        self._exchange(self.part_keys[:keys.numel()], rk, in_splits, out_splits, biggest)
         rps = []
         for src, dstbuf in zip(self.part_pays, self.recv_pays):
             rp = dstbuf[:total]
-            dist.all_to_all_single(_comm(rp), _comm(src[:keys.numel()]), out_splits, in_splits,
-                                   group=self.group)
+            self._exchange(src[:keys.numel()], rp, in_splits, out_splits, biggest)
             rps.append(rp)
         # 6: local sort of the received slice
         self.ops.sort(rk, rps)

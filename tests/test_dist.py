@@ -83,7 +83,8 @@ def _run(rank, world, kind, n_per, dist_kind, q):
             k = np.full(n, 7, dtype=ut)
         keys = torch.from_numpy(k.copy())
         pay = torch.from_numpy(np.arange(n, dtype=np.int64) + rank * 10**9)
-        sorter = ShardSorter(NumpyShardOps(kind), n, [torch.int64], keys.dtype, "cpu", bits=8)
+        sorter = ShardSorter(NumpyShardOps(kind), n, [torch.int64], keys.dtype, "cpu", bits=8,
+                             chunk_bytes=1024)  # many exchange rounds
         ok, (op,) = sorter.sort(keys, [pay])
         mine = ok.numpy().copy()
         u = transformed_keys(kind, True, mine)

@@ -297,3 +297,31 @@ def test_key_histogram_and_partition(kind):
         order = np.argsort(dest, kind="stable")  # stable partition
         assert bytes_equal(ko.cpu().numpy(), keys.cpu().numpy()[order])
         assert bytes_equal(po.cpu().numpy(), pay_h[order])
+
+
+def test_shard_sorter_rccl_world1():
+    """The multi-GPU protocol end to end on one GPU (RCCL, world 1):
+    histogram -> balanced split -> partition -> exchange -> local sort equals
+    the plain device sort bit for bit."""
+    torch = _torch()
+    import os
+    import socket
+    import torch.distributed as dist
+    from srs_amd.dist import HipShardOps, ShardSorter
+    n = 3_000_017
+    keys = torch.empty(n, dtype=torch.int64, device="cuda")
+    pay = torch.empty(n, dtype=torch.int64, device="cuda")
+    srs_amd.fill_synthetic_device(keys, pay, seed=7, key_kind=srs_amd.KEY_U64)
+    ko, po = torch.empty_like(keys), torch.empty_like(pay)
+    srs_amd.sort_device(keys, pay, key_kind=srs_amd.KEY_U64, out=(ko, po))
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        sorter = ShardSorter(HipShardOps(srs_amd.KEY_U64), n, [torch.int64], torch.int64, "cuda")
+        rk, (rp,) = sorter.sort(keys, [pay])
+        assert torch.equal(rk, ko) and torch.equal(rp, po)
+    finally:
+        dist.destroy_process_group()

@@ -22,6 +22,8 @@ for s in "$@"; do
     b9full) step bench_1e9_full 900 python bench.py ;;
     c2) step bench_c2 600 python bench.py --config c2 --steps 3 --cpu-sample 0 ;;
     c3) step bench_c3 600 python bench.py --config c3 --steps 3 --cpu-sample 0 ;;
+    shard) step bench_shard 600 python bench.py --shard --steps 3 --cpu-sample 0 ;;
+    shardc2) step bench_shard_c2 600 python bench.py --shard --config c2 --steps 3 --cpu-sample 0 ;;
   esac
 done
 cat gpurun_out/steps.txt
