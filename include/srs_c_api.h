@@ -112,6 +112,22 @@ int srs_sort_aos_device(int64_t num, int key_kind, int up,
                         int64_t cmp_sort_threshold, void* elements,
                         uint32_t elem_size, void* elements_out, void* stream);
 
+/* Sorts each segment [segment_bounds[i], segment_bounds[i+1]) of a device
+ * key column and its payload columns independently, in place, as sub-ranges
+ * of one sort (no n <= threshold rule per segment). segment_bounds is a HOST
+ * array of num_segments + 1 non-decreasing offsets within [0, num]; elements
+ * outside every segment are untouched. known_top_bits: the caller guarantees
+ * that inside each segment all keys agree on their top known_top_bits
+ * transformed bits (0 = no knowledge); those bits are not examined again.
+ * Asynchronous on `stream` (returns once the work is queued). Replaces
+ * calling radix_sort::sort (radixSort.hpp:1780) once per sub-range; the
+ * multi-GPU shard sorts its receive groups with it. */
+int srs_sort_segments_device(int64_t num, int key_kind, int up, void* keys,
+                             int32_t num_payloads, void* const* payloads,
+                             const uint32_t* payload_sizes, int64_t num_segments,
+                             const int64_t* segment_bounds, int32_t known_top_bits,
+                             void* stream);
+
 /* ---- multi-GPU shard primitives (top-radix-bits partition) --
  * A node-wide sort of one array spread over N GPUs: every rank histograms
  * its keys' top bits (srs_key_histogram_device), the histograms are summed

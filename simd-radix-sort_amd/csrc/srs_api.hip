@@ -221,6 +221,9 @@ struct Request {
   void* out_cols[SRS_MAX_PAYLOADS + 1];
   uint32_t widths[SRS_MAX_PAYLOADS + 1];
   int ncols;                         // SoA: 1 + payloads; AoS: 1
+  const int64_t* seg_bounds = nullptr;  // optional: sort [b[i], b[i+1]) independently
+  int64_t nsegs = 0;
+  int known_top_bits = 0;               // every segment's keys agree on these top bits
 };
 
 void key_masks(int kind, int up, SortDesc& d) {
@@ -393,27 +396,68 @@ int run_sort(Workspace* W, const Request& R, hipStream_t st) {
   SortDesc* d_desc = (SortDesc*)W->desc.p;
   launch_set_desc(d, d_desc, st);
 
-  // ---- initial segment -----------------------------------------------------
-  Seg seg0{0, n, d.key_bits, inplace ? BUF_OUT : BUF_IN};
-  const bool to_local = n <= kLocalCap;
-  size_t big_cap = 1024, local_cap = 1024, copy_cap = 1024;
-  SRS_TRY(ensure(W->big[0], big_cap * sizeof(Seg)));
-  SRS_TRY(ensure(W->big[1], big_cap * sizeof(Seg)));
-  SRS_TRY(ensure(W->local, local_cap * sizeof(Seg)));
-  SRS_TRY(ensure(W->local2, local_cap * sizeof(Seg)));
-  SRS_TRY(ensure(W->copy, copy_cap * sizeof(Seg)));
+  // ---- initial segments ----------------------------------------------------
+  const int home = inplace ? BUF_OUT : BUF_IN;
+  SRS_TRY(ensure(W->big[0], 1024 * sizeof(Seg)));
+  SRS_TRY(ensure(W->big[1], 1024 * sizeof(Seg)));
+  SRS_TRY(ensure(W->local, 1024 * sizeof(Seg)));
+  SRS_TRY(ensure(W->local2, 1024 * sizeof(Seg)));
+  SRS_TRY(ensure(W->copy, 1024 * sizeof(Seg)));
   SRS_TRY(ensure(W->ctr, sizeof(ListCounters)));
   SRS_TRY(ensure(W->totals, 4 * sizeof(uint64_t)));
   ListCounters* d_ctr = (ListCounters*)W->ctr.p;
   uint64_t* d_totals = (uint64_t*)W->totals.p;
-  launch_init_lists(seg0, to_local ? 1 : 0, (Seg*)W->big[0].p, (Seg*)W->local.p,
-                    (Seg*)W->local2.p, d_ctr, st);
-
-  int64_t n_local = (to_local && n <= kLocalCapSmall) ? 1 : 0;
-  int64_t n_local2 = (to_local && n > kLocalCapSmall) ? 1 : 0;
-  int64_t n_copy = 0;
-  W->h_ctr->local_elems = to_local ? (uint64_t)n : 0;
-  LevelState S{to_local ? 0 : 1, n_local, n_local2, n_copy, 0};
+  int64_t n_big = 0, n_local = 0, n_local2 = 0, n_copy = 0;
+  if (R.nsegs > 0) {
+    // independent segments (multi-GPU receive groups): sorted as sub-ranges
+    // of one sort, each starting at the full key width (the varying-bit
+    // detection skips what a segment's keys share)
+    std::vector<Seg> hb, hl, hl2;
+    uint64_t lel = 0;
+    for (int64_t i = 0; i < R.nsegs; i++) {
+      const int64_t a = R.seg_bounds[i], len = R.seg_bounds[i + 1] - a;
+      if (len < 2) continue;
+      const Seg g{a, len, d.key_bits - R.known_top_bits, home};
+      if (len <= kLocalCapSmall) hl.push_back(g);
+      else if (len <= kLocalCap) hl2.push_back(g);
+      else hb.push_back(g);
+      if (len <= kLocalCap) lel += (uint64_t)len;
+    }
+    SRS_TRY(ensure(W->big[0], std::max<size_t>(1024, hb.size()) * sizeof(Seg)));
+    SRS_TRY(ensure(W->local, std::max<size_t>(1024, hl.size()) * sizeof(Seg)));
+    SRS_TRY(ensure(W->local2, std::max<size_t>(1024, hl2.size()) * sizeof(Seg)));
+    if (!hb.empty())
+      HIP_TRY(hipMemcpyAsync(W->big[0].p, hb.data(), hb.size() * sizeof(Seg),
+                             hipMemcpyHostToDevice, st));
+    if (!hl.empty())
+      HIP_TRY(hipMemcpyAsync(W->local.p, hl.data(), hl.size() * sizeof(Seg),
+                             hipMemcpyHostToDevice, st));
+    if (!hl2.empty())
+      HIP_TRY(hipMemcpyAsync(W->local2.p, hl2.data(), hl2.size() * sizeof(Seg),
+                             hipMemcpyHostToDevice, st));
+    ListCounters c;
+    memset(&c, 0, sizeof c);
+    c.n_big = hb.size();
+    c.n_local = hl.size();
+    c.n_local2 = hl2.size();
+    c.local_elems = lel;
+    HIP_TRY(hipMemcpyAsync(d_ctr, &c, sizeof c, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipStreamSynchronize(st));  // the host vectors go out of scope
+    n_big = (int64_t)hb.size();
+    n_local = (int64_t)hl.size();
+    n_local2 = (int64_t)hl2.size();
+    W->h_ctr->local_elems = lel;
+  } else {
+    Seg seg0{0, n, d.key_bits, home};
+    const bool to_local = n <= kLocalCap;
+    launch_init_lists(seg0, to_local ? 1 : 0, (Seg*)W->big[0].p, (Seg*)W->local.p,
+                      (Seg*)W->local2.p, d_ctr, st);
+    n_big = to_local ? 0 : 1;
+    n_local = (to_local && n <= kLocalCapSmall) ? 1 : 0;
+    n_local2 = (to_local && n > kLocalCapSmall) ? 1 : 0;
+    W->h_ctr->local_elems = to_local ? (uint64_t)n : 0;
+  }
+  LevelState S{n_big, n_local, n_local2, n_copy, 0};
   int level = 0;
   while (S.nbig > 0) {
     if (++level > 80) return fail(SRS_ERR_INTERNAL, "level limit exceeded");
@@ -511,6 +555,7 @@ int run_partition(Workspace* W, const Request& R, int bits, const int32_t* d_lut
   d.ncols = R.ncols;
   d.digit_lut = d_lut;
   d.lut_shift = d.key_bits - bits;
+  d.lut_bits = bits;
   SRS_TRY(ensure(W->desc, sizeof(SortDesc)));
   SortDesc* d_desc = (SortDesc*)W->desc.p;
   launch_set_desc(d, d_desc, st);
@@ -690,6 +735,32 @@ int srs_sort_soa_device(int64_t num, int key_kind, int up, int64_t cmp_sort_thre
   SRS_TRY(build_soa(R, num, key_kind, up, cmp_sort_threshold, keys, num_payloads, payloads,
                     payload_sizes, keys_out, payloads_out));
   return sort_device(R, (hipStream_t)stream);
+}
+
+int srs_sort_segments_device(int64_t num, int key_kind, int up, void* keys,
+                             int32_t num_payloads, void* const* payloads,
+                             const uint32_t* payload_sizes, int64_t num_segments,
+                             const int64_t* segment_bounds, int32_t known_top_bits,
+                             void* stream) {
+  if (num_segments < 0) return fail(SRS_ERR_INVALID_ARG, "num_segments < 0");
+  if (known_top_bits < 0 || known_top_bits >= 8 * key_size_of(key_kind))
+    return fail(SRS_ERR_INVALID_ARG, "known_top_bits out of range");
+  if (num_segments > 0 && !segment_bounds) return fail(SRS_ERR_INVALID_ARG, "segment_bounds is NULL");
+  for (int64_t i = 0; i < num_segments; i++)
+    if (segment_bounds[i] < 0 || segment_bounds[i] > segment_bounds[i + 1] ||
+        segment_bounds[i + 1] > num)
+      return fail(SRS_ERR_INVALID_ARG, "segment_bounds must be non-decreasing within [0, num]");
+  Request R;
+  SRS_TRY(build_soa(R, num, key_kind, up, 0, keys, num_payloads, payloads, payload_sizes,
+                    nullptr, nullptr));
+  if (num_segments == 0 || num <= 1) return SRS_OK;
+  R.seg_bounds = segment_bounds;
+  R.nsegs = num_segments;
+  R.known_top_bits = known_top_bits;
+  std::lock_guard<std::mutex> lk(g_wmu);
+  Workspace* W = nullptr;
+  SRS_TRY(get_ws(&W));
+  return run_sort(W, R, (hipStream_t)stream);
 }
 
 int srs_sort_aos_device(int64_t num, int key_kind, int up, int64_t cmp_sort_threshold,

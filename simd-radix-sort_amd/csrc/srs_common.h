@@ -43,6 +43,7 @@ struct SortDesc {
   // partition passes only: digit = digit_lut[u >> lut_shift]
   const int32_t* digit_lut;
   int32_t lut_shift;
+  int32_t lut_bits;   // table size 2^lut_bits; staged in LDS when <= kLdsLutBits
   unsigned long long* stamp_acc;  // diagnostic builds only (SRS_STAMPS)
 };
 
@@ -89,7 +90,7 @@ struct ListCounters {
 #define SRS_SCATTER_ITEMS 4
 #endif
 #ifndef SRS_SCATTER_WAVES_PER_EU
-#define SRS_SCATTER_WAVES_PER_EU 4
+#define SRS_SCATTER_WAVES_PER_EU 8
 #endif
 #ifndef SRS_SCATTER_PIPE
 #define SRS_SCATTER_PIPE 0
@@ -120,6 +121,7 @@ constexpr int kMaxBins = 1 << kMaxDigitBits;   // histogram row stride (tile-maj
 static_assert(kScatterThreads >= kMaxBins, "the scatter tile scan gives one bin per thread");
 constexpr int kScanGroup = 256;                 // tiles per column-scan group
 constexpr int kHistMaxBits = 12;                // srs_key_histogram_device
+constexpr int kLdsLutBits = 12;                 // digit tables up to 16 KB live in LDS
 
 // local sort classes: fast kernel (atomic bucket pass + rank) in two sizes,
 // then the stable kernel and the LSD kernel as fallbacks (same capacity as

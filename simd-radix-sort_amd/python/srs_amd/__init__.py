@@ -61,6 +61,8 @@ def lib() -> ctypes.CDLL:
     L.srs_sort_soa_device.argtypes = [i64, ctypes.c_int, ctypes.c_int, i64, vp, i32, vp, vp,
                                       vp, vp, vp]
     L.srs_sort_aos_device.argtypes = [i64, ctypes.c_int, ctypes.c_int, i64, vp, u32, vp, vp]
+    L.srs_sort_segments_device.argtypes = [i64, ctypes.c_int, ctypes.c_int, vp, i32, vp, vp, i64,
+                                           vp, i32, vp]
     L.srs_fill_synthetic_device.argtypes = [i64, ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64,
                                             vp, i32, vp, vp, vp]
     L.srs_key_histogram_device.argtypes = [i64, ctypes.c_int, ctypes.c_int, vp, ctypes.c_int, vp,
@@ -187,6 +189,23 @@ def sort_device(keys, *payloads, up: bool = True, cmp_sort_threshold: int = 16,
     _check(lib().srs_sort_soa_device(keys.numel(), kind, int(bool(up)), int(cmp_sort_threshold),
                                      keys.data_ptr(), np_, pays, sizes, kout, pout,
                                      _stream_ptr(stream)))
+
+
+def sort_segments_device(keys, *payloads, bounds, up: bool = True, key_kind: int | None = None,
+                         known_top_bits: int = 0, stream=None) -> None:
+    """Sort every segment [bounds[i], bounds[i+1]) of the device columns
+    independently, in place (srs_sort_segments_device). `bounds`: host
+    sequence of non-decreasing offsets; `known_top_bits`: top transformed
+    key bits every segment's keys are known to share."""
+    for t in (keys,) + payloads:
+        if not (t.is_cuda and t.is_contiguous() and t.dim() == 1 and t.numel() == keys.numel()):
+            raise ValueError("tensors must be 1-D contiguous device tensors of equal length")
+    kind = _torch_kind(keys) if key_kind is None else int(key_kind)
+    b = (ctypes.c_int64 * len(bounds))(*[int(x) for x in bounds])
+    _check(lib().srs_sort_segments_device(
+        keys.numel(), kind, int(bool(up)), keys.data_ptr(), len(payloads),
+        _ptr_array([p.data_ptr() for p in payloads]), _size_array([p.element_size() for p in payloads]),
+        max(0, len(bounds) - 1), b, int(known_top_bits), _stream_ptr(stream)))
 
 
 def sort_combined_device(elements, key_kind: int, up: bool = True,

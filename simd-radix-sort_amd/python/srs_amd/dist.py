@@ -1,24 +1,29 @@
 """Multi-GPU shard sort: one array spread over N GPUs (one process per GPU,
-torch.distributed over RCCL/xGMI), sorted by its top radix bits.
+torch.distributed over RCCL/xGMI), sorted across the GPUs.
 
-Protocol, per rank r holding n_r keys (+ payload columns):
-  1. histogram of the transformed top `bits` key bits   (srs_key_histogram_device)
-  2. all-reduce of the 2^bits histogram                  (RCCL, 32 KB at 12 bits)
-  3. bucket -> rank map: contiguous bucket ranges with ~equal key counts
-  4. stable partition of the local columns by destination rank
-                                                         (srs_partition_device)
-  5. all-gather of the group sizes, then every column moves peer to peer
-     (batched isend/irecv = RCCL's grouped send/recv over xGMI), in rounds
-     of at most 256 MB per message: RCCL corrupted a single 8 GB message
-     (measured: all_to_all_single of 1e9 int64 at world 1; 1e8 was exact)
-  6. local sort of what was received                     (srs_sort_soa_device)
-Rank r then holds the r-th contiguous slice of the globally sorted array:
-every key on rank r orders before every key on rank r+1.
+Protocol, per rank r holding n_r records (key + payload columns):
+  1. histogram of the transformed top `bits` key bits    (srs_key_histogram_device)
+  2. all-reduce of the 2^bits histogram                   (RCCL, 32 KB at 12 bits)
+  3. bins -> G (<= 512) key-range groups of ~equal size; contiguous runs of
+     groups -> ranks, again balanced by size
+  4. stable partition of the local records into the G groups
+                                                          (srs_partition_device)
+     This IS the first MSB level of the sort: nothing is partitioned twice.
+  5. all-gather of the G group sizes of every rank; each rank lays out its
+     receive buffer group by group (sources in rank order inside a group),
+     so what arrives is already grouped by key range
+  6. the groups move peer to peer (batched isend/irecv = RCCL grouped
+     send/recv over xGMI) in `rounds`, every message <= 256 MB (RCCL
+     corrupted a single 8 GB all_to_all message: measured at world 1, 1e9
+     int64; 1e8 was exact). While round i+1 is in flight, the groups of
+     round i are sorted on a second stream    (srs_sort_segments_device)
+Rank r then holds the r-th slice of the globally sorted array: every key on
+rank r orders before every key on rank r+1.
 
-The device work goes through an `ops` backend (ShardOps) so that the same
-protocol code runs on CPU under gloo in the tests (NumpyShardOps in
-tests/test_dist.py) and on MI355X under RCCL (HipShardOps, the product path).
-The reference (jonicho/simd-radix-sort) has no multi-device path.
+The device work goes through an `ops` backend so that the same protocol code
+runs on CPU under gloo in the tests (NumpyShardOps in tests/test_dist.py) and
+on MI355X under RCCL (HipShardOps, the product path). The reference
+(jonicho/simd-radix-sort) has no multi-device path.
 """
 from __future__ import annotations
 
@@ -27,9 +32,9 @@ import torch.distributed as dist
 
 
 def balanced_split(hist: torch.Tensor, world: int) -> torch.Tensor:
-    """Bucket -> rank map (int32, non-decreasing) giving each rank a contiguous
-    range of buckets holding ~total/world keys: bucket b goes to rank
-    floor(world * (keys before b + half of b) / total)."""
+    """Bucket -> part map (int32, non-decreasing) giving each of `world`
+    parts a contiguous range of buckets holding ~total/world keys: bucket b
+    goes to part floor(world * (keys before b + half of b) / total)."""
     h = hist.to(torch.float64)
     total = float(h.sum().item())
     if total <= 0:
@@ -57,6 +62,7 @@ class HipShardOps:
         import srs_amd
         self.srs = srs_amd
         self.kind = kind
+        self.stream = None
 
     def histogram(self, keys, bits):
         h = torch.zeros(1 << bits, dtype=torch.int64, device=keys.device)
@@ -70,27 +76,45 @@ class HipShardOps:
     def sort(self, keys, pays):
         self.srs.sort_device(keys, *pays, key_kind=self.kind)
 
+    def sort_segments(self, keys, pays, bounds, known_top_bits=0):
+        """Queue the sort of the given segments on a side stream, after the
+        work already queued on the current stream (the receives)."""
+        if self.stream is None:
+            self.stream = torch.cuda.Stream(device=keys.device)
+        self.stream.wait_stream(torch.cuda.current_stream(keys.device))
+        self.srs.sort_segments_device(keys, *pays, bounds=bounds, key_kind=self.kind,
+                                      known_top_bits=known_top_bits, stream=self.stream)
+
+    def finish(self, device):
+        if self.stream is not None:
+            torch.cuda.current_stream(device).wait_stream(self.stream)
+
 
 class ShardSorter:
     """Sorts the union of every rank's (keys, payloads) across the process
-    group. Buffers are allocated once (capacity = slack * n per rank)."""
+    group. Buffers are allocated once (receive capacity = slack * n per rank)
+    and grown if a rank receives more."""
 
     def __init__(self, ops, n_local: int, payload_dtypes, key_dtype, device, bits: int = 12,
-                 slack: float = 1.25, group=None, chunk_bytes: int = 256 << 20):
+                 groups: int = 512, rounds: int = 4, slack: float = 1.25, group=None,
+                 chunk_bytes: int = 256 << 20):
         self.ops = ops
-        self.bits = bits
+        self.key_bits = 8 * torch.empty(0, dtype=key_dtype).element_size()
+        self.bits = min(bits, self.key_bits)
+        self.groups = min(groups, 512, 1 << bits)
+        self.rounds = max(1, rounds)
         self.group = group
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
         self.device = device
         self.n = n_local
+        self.chunk_bytes = chunk_bytes
         cap = int(n_local * slack) + 1024
         self.part_keys = torch.empty(n_local, dtype=key_dtype, device=device)
         self.part_pays = [torch.empty(n_local, dtype=dt, device=device) for dt in payload_dtypes]
         self.recv_keys = torch.empty(cap, dtype=key_dtype, device=device)
         self.recv_pays = [torch.empty(cap, dtype=dt, device=device) for dt in payload_dtypes]
         self.last_counts = None
-        self.chunk_bytes = chunk_bytes
 
     def _ensure_capacity(self, total):
         if total <= self.recv_keys.numel():
@@ -100,73 +124,106 @@ class ShardSorter:
         self.recv_pays = [torch.empty(cap, dtype=p.dtype, device=self.device)
                           for p in self.recv_pays]
 
-    def _exchange(self, send, recv, in_splits, out_splits, biggest):
-        """send: groups by destination rank; recv: groups by source rank.
-        The own group is a local copy; the others move in rounds of at most
-        `chunk_bytes` per message, every rank running the same rounds."""
-        w, me = self.world, self.rank
-        soff = [0] * w
-        roff = [0] * w
-        for i in range(1, w):
-            soff[i] = soff[i - 1] + in_splits[i - 1]
-            roff[i] = roff[i - 1] + out_splits[i - 1]
-        if in_splits[me]:
-            recv[roff[me]:roff[me] + in_splits[me]].copy_(send[soff[me]:soff[me] + in_splits[me]])
-        if w == 1:
-            return
-        C = max(1, self.chunk_bytes // send.element_size())
-        rounds = (biggest + C - 1) // C
-        s_c, r_c = _comm(send), _comm(recv)
-        for r in range(rounds):
-            a = r * C
-            ops = []
-            for peer in range(w):
-                if peer == me:
-                    continue
-                ls = min(C, in_splits[peer] - a)
-                if ls > 0:
-                    ops.append(dist.P2POp(dist.isend, s_c[soff[peer] + a:soff[peer] + a + ls], peer,
-                                          group=self.group))
-                lr = min(C, out_splits[peer] - a)
-                if lr > 0:
-                    ops.append(dist.P2POp(dist.irecv, r_c[roff[peer] + a:roff[peer] + a + lr], peer,
-                                          group=self.group))
-            if ops:
-                for req in dist.batch_isend_irecv(ops):
-                    req.wait()
+    def plan(self, hist):
+        """bins -> groups (device int32, for the partition) and groups -> ranks
+        (host list), both non-decreasing."""
+        G, w = self.groups, self.world
+        group_of_bin = balanced_split(hist, G)
+        gtot = torch.zeros(G, dtype=torch.int64, device=hist.device)
+        gtot.index_add_(0, group_of_bin.to(torch.int64), hist.to(torch.int64))
+        rank_of_group = balanced_split(gtot, w).tolist()
+        # top key bits shared inside each group: the common prefix of its
+        # first and last bin
+        gb = group_of_bin.tolist()
+        first, last = [None] * G, [None] * G
+        for b, g in enumerate(gb):
+            if first[g] is None:
+                first[g] = b
+            last[g] = b
+        prefix = [0 if first[g] is None else self.bits - (first[g] ^ last[g]).bit_length()
+                  for g in range(G)]
+        return group_of_bin, rank_of_group, prefix
 
     def sort(self, keys, pays):
         """Returns (keys, payloads) views: this rank's slice of the sorted union."""
-        w = self.world
-        if keys.numel() > self.part_keys.numel():
-            self.part_keys = torch.empty(keys.numel(), dtype=keys.dtype, device=self.device)
-            self.part_pays = [torch.empty(keys.numel(), dtype=p.dtype, device=self.device)
+        w, me, G, R = self.world, self.rank, self.groups, self.rounds
+        n = keys.numel()
+        if n > self.part_keys.numel():
+            self.part_keys = torch.empty(n, dtype=keys.dtype, device=self.device)
+            self.part_pays = [torch.empty(n, dtype=p.dtype, device=self.device)
                               for p in self.part_pays]
-        # 1-3: global histogram -> contiguous bucket ranges per rank
+        # 1-3: global histogram -> key-range groups -> ranks
         hist = self.ops.histogram(keys, self.bits)
         dist.all_reduce(hist, group=self.group)
-        part_of_bucket = balanced_split(hist, w)
-        # 4: stable partition by destination rank
-        counts = self.ops.partition(keys, pays, self.bits, part_of_bucket, w,
+        group_of_bin, rank_of_group, prefix = self.plan(hist)
+        # 4: stable partition into the groups (the first radix level)
+        counts = self.ops.partition(keys, pays, self.bits, group_of_bin, G,
                                     (self.part_keys, *self.part_pays))
-        # 5: exchange sizes (full matrix, so every rank agrees on the rounds)
+        # 5: everyone's group sizes -> receive layout
         send = torch.tensor(counts, dtype=torch.int64, device=hist.device)
         mat = [torch.empty_like(send) for _ in range(w)]
         dist.all_gather(mat, send, group=self.group)
-        mat = [m.tolist() for m in mat]           # mat[src][dst]
-        in_splits = [int(c) for c in counts]
-        out_splits = [int(mat[src][self.rank]) for src in range(w)]
-        total = sum(out_splits)
+        mat = [m.tolist() for m in mat]                   # mat[src][g]
+        owned = [[g for g in range(G) if rank_of_group[g] == r] for r in range(w)]
+        rnd = [0] * G                                     # exchange round of each group
+        for r in range(w):
+            for i, g in enumerate(owned[r]):
+                rnd[g] = i * R // max(1, len(owned[r]))
+        soff = [0] * (G + 1)
+        for g in range(G):
+            soff[g + 1] = soff[g] + counts[g]
+        roff = {}                                         # (g, src) -> receive offset
+        gbound = {}                                       # g -> (start, end) in recv
+        pos = 0
+        for g in owned[me]:
+            start = pos
+            for src in range(w):
+                roff[(g, src)] = pos
+                pos += mat[src][g]
+            gbound[g] = (start, pos)
+        total = pos
         self._ensure_capacity(total)
-        biggest = max(max(row) for row in mat)
         rk = self.recv_keys[:total]
-        self._exchange(self.part_keys[:keys.numel()], rk, in_splits, out_splits, biggest)
-        rps = []
-        for src, dstbuf in zip(self.part_pays, self.recv_pays):
-            rp = dstbuf[:total]
-            self._exchange(src[:keys.numel()], rp, in_splits, out_splits, biggest)
-            rps.append(rp)
-        # 6: local sort of the received slice
-        self.ops.sort(rk, rps)
-        self.last_counts = (in_splits, out_splits)
+        rps = [b[:total] for b in self.recv_pays]
+        cols = [(self.part_keys, rk)] + list(zip(self.part_pays, rps))
+        # 6: rounds of peer-to-peer moves; sort each round's groups meanwhile
+        for r in range(R):
+            p2p = []
+            for g in range(G):
+                if rnd[g] != r:
+                    continue
+                dst = rank_of_group[g]
+                if dst == me:
+                    for src in range(w):
+                        cnt = mat[src][g]
+                        if cnt == 0:
+                            continue
+                        a = roff[(g, src)]
+                        for sbuf, rbuf in cols:
+                            if src == me:
+                                rbuf[a:a + cnt].copy_(sbuf[soff[g]:soff[g] + cnt])
+                            else:
+                                self._msgs(p2p, dist.irecv, rbuf, a, cnt, src)
+                elif counts[g]:
+                    for sbuf, _ in cols:
+                        self._msgs(p2p, dist.isend, sbuf, soff[g], counts[g], dst)
+            if p2p:
+                for req in dist.batch_isend_irecv(p2p):
+                    req.wait()
+            mine = [g for g in owned[me] if rnd[g] == r]
+            if mine:
+                bounds = [gbound[mine[0]][0]] + [gbound[g][1] for g in mine]
+                known = min(min(prefix[g] for g in mine), self.key_bits - 1)
+                self.ops.sort_segments(rk, rps, bounds, known)
+        self.ops.finish(self.device)
+        self.last_counts = (counts, [sum(mat[s][g] for g in owned[me]) for s in range(w)])
         return rk, rps
+
+    def _msgs(self, p2p, op, buf, off, cnt, peer):
+        """One message per <= chunk_bytes piece (sender and receiver split a
+        group the same way, so the pieces pair up in order)."""
+        C = max(1, self.chunk_bytes // buf.element_size())
+        v = _comm(buf)
+        for a in range(0, cnt, C):
+            b = min(cnt, a + C)
+            p2p.append(dist.P2POp(op, v[off + a:off + b], peer, group=self.group))

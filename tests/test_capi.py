@@ -67,3 +67,43 @@ def test_argument_validation_without_gpu():
     assert lib.srs_sort_soa(1, 4, 1, 16, k.ctypes.data, 0, None, None) == 0
     assert lib.srs_sort_soa(-5, 4, 1, 16, k.ctypes.data, 0, None, None) == 0
     assert srs_amd.version().startswith("srs_amd")
+
+
+def _kernel_resources():
+    """Per-kernel VGPRs / scratch / occupancy from the build's compiler
+    remarks (simd-radix-sort_amd/build/srs_kernels.remarks)."""
+    path = os.path.join(REPO, "simd-radix-sort_amd", "build", "srs_kernels.remarks")
+    if not os.path.exists(path):
+        pytest.skip("no resource remarks (library built elsewhere)")
+    res, cur = {}, None
+    for line in open(path):
+        m = re.search(r"Function Name: (\S+)", line)
+        if m:
+            cur = m.group(1)
+            res[cur] = {}
+            continue
+        m = re.search(r"(VGPRs|ScratchSize \[bytes/lane\]|Occupancy \[waves/SIMD\]|"
+                      r"LDS Size \[bytes/block\]): (\d+)", line)
+        if m and cur:
+            res[cur][m.group(1).split()[0]] = int(m.group(2))
+    return res
+
+
+def test_hot_kernels_keep_their_occupancy():
+    """The occupancy the tuning relies on: two 16-wave scatter
+    workgroups per CU need <= 64 VGPRs (8 waves/SIMD); count 8 waves/SIMD;
+    the small local class 6 waves/SIMD (3 workgroups of 8 waves); nothing
+    on the hot path spills to scratch."""
+    res = _kernel_resources()
+    need = {"scatter_kernel": 8, "count_kernel": 8, "local_kernelI": None}
+    seen = set()
+    for name, r in res.items():
+        for key, occ in need.items():
+            if key not in name:
+                continue
+            seen.add(key)
+            assert r.get("ScratchSize", 0) == 0, (name, r)
+            if key == "local_kernelI":
+                occ = 6 if "Li512ELi8ELi6E" in name else 4
+            assert r["Occupancy"] >= occ, (name, r)
+    assert seen == set(need)

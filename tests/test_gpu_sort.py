@@ -325,3 +325,42 @@ def test_shard_sorter_rccl_world1():
         assert torch.equal(rk, ko) and torch.equal(rp, po)
     finally:
         dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("kind", [6, 8, 3], ids=lambda k: KIND_NAMES[k])
+def test_sort_segments_device(kind):
+    """srs_sort_segments_device: every segment sorted on its own (stable),
+    bytes outside the segments untouched; sizes span the local and global
+    paths."""
+    torch = _torch()
+    rng = np.random.default_rng(5)
+    lens = [0, 1, 2, 17, 4096, 4097, 8192, 8193, 50_000, 300_001, 3]
+    gaps = [5, 0, 3, 0, 0, 1, 0, 7, 0, 2, 0]
+    pos, segs = 0, []
+    for ln, gp in zip(lens, gaps):
+        pos += gp
+        segs.append((pos, pos + ln))
+        pos += ln
+    n = pos + 11
+    keys_h = make_keys(kind, "uniform", n, kind)
+    pay_h = np.arange(n, dtype=np.int64)
+    keys = torch.from_numpy(keys_h.view(np.int64) if kind == 6 else keys_h).cuda()
+    pay = torch.from_numpy(pay_h).cuda()
+    # bounds list every segment's ends; the stretches between listed
+    # segments are segments too, and [0, 5) and the last 11 are outside all
+    flat = []
+    for a, b in segs:
+        flat += [a, b]
+    srs_amd.sort_segments_device(keys, pay, bounds=flat, key_kind=kind)
+    ko = keys.cpu().numpy().view(keys_h.dtype)
+    po = pay.cpu().numpy()
+    exp_k, exp_p = keys_h.copy(), pay_h.copy()
+    edges = list(zip(flat[:-1], flat[1:]))  # every consecutive pair is a segment
+    for a, b in edges:
+        if b - a < 2:
+            continue
+        u = transformed_keys(kind, True, keys_h[a:b])
+        o = np.argsort(u, kind="stable")
+        exp_k[a:b] = keys_h[a:b][o]
+        exp_p[a:b] = pay_h[a:b][o]
+    assert bytes_equal(ko, exp_k) and np.array_equal(po, exp_p)
