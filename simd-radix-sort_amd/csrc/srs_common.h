@@ -144,10 +144,14 @@ constexpr int kLocalCapSmall = kLocalThreadsSmall * kLocalItemsSmall;  // 4096
 // occupancy the LDS footprint allows (90 KB -> 1 block/CU; 49 KB -> 3 blocks/CU)
 constexpr int kLocalWavesPerEU = kLocalThreads / 64 / 4;
 constexpr int kLocalWavesPerEUSmall = 3 * kLocalThreadsSmall / 64 / 4;
-constexpr int kLocalStableThreads = 512;
-constexpr int kLocalStableItems = 16;
+#ifndef SRS_LOCAL_STABLE_ITEMS
+#define SRS_LOCAL_STABLE_ITEMS 8
+#endif
+constexpr int kLocalStableItems = SRS_LOCAL_STABLE_ITEMS;
+constexpr int kLocalStableThreads = kLocalCap / kLocalStableItems;
+constexpr int kLocalStableThreadsSmall = kLocalCapSmall / kLocalStableItems;
 static_assert(kLocalStableThreads * kLocalStableItems == kLocalCap, "fallback capacity");
-static_assert(kLocalStableThreads / 2 * kLocalStableItems == kLocalCapSmall, "fallback capacity");
+static_assert(kLocalStableThreadsSmall * kLocalStableItems == kLocalCapSmall, "fallback capacity");
 constexpr int kLocalTarget = 6144;                        // digit sizing target
 
 }  // namespace srs

@@ -958,8 +958,8 @@ __device__ __forceinline__ void local_digit_pass(
     U* su, uint16_t* sidx, uint16_t (*wc)[1 << kLocalBits], uint32_t* bin_start,
     uint32_t* scan_sh) {
   constexpr int NW = NT / 64;
-  constexpr int BPT = (1 << kLocalBits) / NT;  // bins per thread
-  static_assert(BPT >= 1 && BPT * NT == (1 << kLocalBits), "bins per thread");
+  constexpr int BPT = (1 << kLocalBits) >= NT ? (1 << kLocalBits) / NT : 1;  // bins per thread
+  static_assert(BPT * NT >= (1 << kLocalBits), "bins per thread");
   const uint32_t wave = threadIdx.x >> 6;
   const uint32_t nb = 1u << nbits, mask = nb - 1;
   for (uint32_t i = threadIdx.x; i < (uint32_t)(NW << kLocalBits); i += NT) (&wc[0][0])[i] = 0;
@@ -1264,10 +1264,10 @@ __global__ __launch_bounds__(NT) void local_stable_kernel(
   constexpr int NB = 1 << kLocalTopBits;
   constexpr int BPT = NB / NT;
   static_assert(BPT >= 1 && BPT * NT == NB, "bins per thread");
-  static_assert(NW * NB == CAP, "ballot counters and the permutation share storage");
+  constexpr int WCP = NW * NB > CAP ? NW * NB : CAP;
   // sbuf: packed sort words during the sort, column staging afterwards
   __shared__ uint64_t sbuf[CAP];
-  __shared__ uint16_t wc_perm[CAP];       // ballot counters [NW][NB], then perm[CAP]
+  __shared__ uint16_t wc_perm[WCP];       // ballot counters [NW][NB], then perm[CAP]
   __shared__ uint32_t bflag[NB];          // bucket holds differing keys
   __shared__ uint32_t bin_start[NB + 1];
   __shared__ uint32_t scan_sh[NW + 1];
@@ -1294,7 +1294,7 @@ __global__ __launch_bounds__(NT) void local_stable_kernel(
     sh_or = 0;
     maxlen = 0;
   }
-  for (uint32_t i = threadIdx.x; i < (uint32_t)CAP; i += NT) wc_perm[i] = 0;
+  for (uint32_t i = threadIdx.x; i < (uint32_t)WCP; i += NT) wc_perm[i] = 0;
   for (uint32_t i = threadIdx.x; i < (uint32_t)NB; i += NT) bflag[i] = 0;
 
   // ---- 1. keys (column 0 holds the key in its low bytes) -------------------
@@ -1748,8 +1748,8 @@ void launch_local_stable(int key_size, const SortDesc* d, const Seg* segs,
         <<<(unsigned)grid, kLocalStableThreads, 0, st>>>(d, segs, nsegs, fallback,      \
                                                          fallback_count);              \
   else                                                                                 \
-    local_stable_kernel<KT, U, kLocalStableThreads / 2>                                \
-        <<<(unsigned)grid, kLocalStableThreads / 2, 0, st>>>(d, segs, nsegs, fallback,  \
+    local_stable_kernel<KT, U, kLocalStableThreadsSmall>                               \
+        <<<(unsigned)grid, kLocalStableThreadsSmall, 0, st>>>(d, segs, nsegs, fallback, \
                                                              fallback_count)
   SRS_KEY_DISPATCH(key_size, CALL)
 #undef CALL
