@@ -62,6 +62,16 @@ struct DataElement<K> {
 // (radixSort.hpp:159-178) becomes the GPU's LDS-resident leaf; the name is
 // kept so that existing call sites compile unchanged.
 struct CmpSorterInsertionSort {};
+// src/cmp_sorters.hpp:66-78: the reference leaves every leaf (<= threshold
+// elements) in partition order, so each element ends within
+// cmpSortThreshold of its sorted position. A leaf holds exactly the elements
+// a full sort puts there; the GPU sorts the leaves anyway (its LDS pass
+// sorts whole segments at once), which meets the same guarantee.
+struct CmpSorterNoSort {};
+// src/cmp_sorters.hpp:40-63 (needs the vendored bramas sorters there): the
+// leaves are sorted (as here); the reference's type restrictions are kept
+// as compile-time errors below.
+struct CmpSorterBramasSmallSort {};
 
 namespace radix_sort {
 
@@ -94,6 +104,30 @@ constexpr int key_kind() {
   else return -1;
 }
 
+template <typename CmpSorter>
+inline constexpr bool known_cmp_sorter = std::is_same_v<CmpSorter, CmpSorterInsertionSort> ||
+                                         std::is_same_v<CmpSorter, CmpSorterNoSort> ||
+                                         std::is_same_v<CmpSorter, CmpSorterBramasSmallSort>;
+
+template <typename BitSorter>
+inline constexpr bool known_bit_sorter = std::is_same_v<BitSorter, BitSorterSIMD> ||
+                                         std::is_same_v<BitSorter, BitSorterSequential>;
+
+// src/cmp_sorters.hpp:47-61
+template <bool Up, typename CmpSorter, typename K, typename... Ps>
+constexpr void check_cmp_sorter() {
+  static_assert(known_cmp_sorter<CmpSorter>,
+                "CmpSorter must be CmpSorterInsertionSort, CmpSorterNoSort or "
+                "CmpSorterBramasSmallSort (a user-defined leaf sorter cannot run on the GPU)");
+  if constexpr (std::is_same_v<CmpSorter, CmpSorterBramasSmallSort>) {
+    static_assert(std::is_same_v<K, double> || std::is_same_v<K, int>,
+                  "BramasSmallSort only supports int and double");
+    static_assert(Up, "BramasSmallSort only supports sorting up");
+    static_assert(sizeof...(Ps) <= 1, "BramasSmallSort only supports one or zero payloads");
+    static_assert(((std::is_same_v<K, Ps>) && ...), "key and payload must have the same type");
+  }
+}
+
 template <typename T>
 inline constexpr bool valid_payload =
     std::is_trivially_copyable_v<T> &&
@@ -113,6 +147,9 @@ inline void check(int rc, const char* what) {
 template <bool Up, typename BitSorter, typename CmpSorter, typename K, typename... Ps>
 void sort(SortIndex cmpSortThreshold, const SortIndex num, K* const keys,
           Ps* const... payloads) {
+  static_assert(detail::known_bit_sorter<BitSorter>,
+                "BitSorter must be BitSorterSIMD or BitSorterSequential");
+  detail::check_cmp_sorter<Up, CmpSorter, K, Ps...>();
   static_assert(detail::key_kind<K>() >= 0,
                 "key type must be one of u8/i8/u16/i16/u32/i32/u64/i64/float/double");
   static_assert((detail::valid_payload<Ps> && ...),
@@ -130,6 +167,11 @@ void sort(SortIndex cmpSortThreshold, const SortIndex num, K* const keys,
 template <bool Up, typename BitSorter, typename CmpSorter, typename K, typename... Ps>
 void sort(SortIndex cmpSortThreshold, const SortIndex num,
           DataElement<K, Ps...>* const elements) {
+  static_assert(detail::known_bit_sorter<BitSorter>,
+                "BitSorter must be BitSorterSIMD or BitSorterSequential");
+  static_assert(detail::known_cmp_sorter<CmpSorter>,
+                "CmpSorter must be CmpSorterInsertionSort, CmpSorterNoSort or "
+                "CmpSorterBramasSmallSort (a user-defined leaf sorter cannot run on the GPU)");
   static_assert(is_power_of_two<sizeof(DataElement<K, Ps...>)>,
                 "size of DataElement<K, Ps...> must be a power of two");
   static_assert(sizeof(DataElement<K, Ps...>) <= 64, "DataElement larger than 64 bytes");

@@ -34,6 +34,47 @@ def test_dropin_rejects_non_power_of_two_element_at_compile_time():
     assert r.returncode != 0 and b"power of two" in r.stderr
 
 
+def _compile(src):
+    return subprocess.run(["g++", "-std=c++17", "-fsyntax-only", "-x", "c++",
+                           "-I", os.path.join(REPO, "include"), "-"], input=src.encode(),
+                          capture_output=True)
+
+
+def test_dropin_accepts_every_reference_sorter_tag():
+    """src/cmp_sorters.hpp's three leaf sorters and both bit sorters."""
+    src = ('#include "simd_sort/radix_sort.hpp"\n'
+           "using namespace simd_sort;\n"
+           "int main(){ double k[4]={3,1,2,0}; double p[4]={0,1,2,3}; int i[4]={4,3,2,1};\n"
+           " radix_sort::sort<true, radix_sort::BitSorterSIMD, CmpSorterNoSort>(16, 4, k, p);\n"
+           " radix_sort::sort<true, radix_sort::BitSorterSequential, CmpSorterInsertionSort>(16, 4, k);\n"
+           " radix_sort::sort<true, radix_sort::BitSorterSIMD, CmpSorterBramasSmallSort>(16, 4, k, p);\n"
+           " radix_sort::sort<true, radix_sort::BitSorterSIMD, CmpSorterBramasSmallSort>(16, 4, i);\n"
+           " DataElement<unsigned, unsigned> e[2]{};\n"
+           " radix_sort::sort<false, radix_sort::BitSorterSIMD, CmpSorterNoSort>(16, 2, e);\n"
+           " return 0; }\n")
+    r = _compile(src)
+    assert r.returncode == 0, r.stderr.decode()[-2000:]
+
+
+@pytest.mark.parametrize("call,msg", [
+    ("radix_sort::sort<true, radix_sort::BitSorterSIMD, CmpSorterBramasSmallSort>(16, 4, f)",
+     "only supports int and double"),
+    ("radix_sort::sort<false, radix_sort::BitSorterSIMD, CmpSorterBramasSmallSort>(16, 4, k)",
+     "only supports sorting up"),
+    ("radix_sort::sort<true, radix_sort::BitSorterSIMD, CmpSorterBramasSmallSort>(16, 4, k, f)",
+     "same type"),
+    ("radix_sort::sort<true, radix_sort::BitSorterSIMD, MySorter>(16, 4, k)",
+     "user-defined leaf sorter"),
+])
+def test_dropin_rejects_what_the_reference_rejects(call, msg):
+    src = ('#include "simd_sort/radix_sort.hpp"\n'
+           "using namespace simd_sort; struct MySorter {};\n"
+           "int main(){ double k[4]={3,1,2,0}; float f[4]={0,1,2,3};\n "
+           + call + "; return 0; }\n")
+    r = _compile(src)
+    assert r.returncode != 0 and msg.encode() in r.stderr, r.stderr.decode()[-1500:]
+
+
 @pytest.mark.gpu
 def test_dropin_matrix_on_gpu():
     if not os.path.exists(BIN):
