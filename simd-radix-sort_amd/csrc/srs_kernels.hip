@@ -58,6 +58,14 @@ __device__ __forceinline__ void stw(char* p, uint64_t v) {
 }
 
 template <int W>
+__device__ __forceinline__ void stw_nt(char* p, uint64_t v) {
+  if constexpr (W == 1) __builtin_nontemporal_store((uint8_t)v, (uint8_t*)p);
+  else if constexpr (W == 2) __builtin_nontemporal_store((uint16_t)v, (uint16_t*)p);
+  else if constexpr (W == 4) __builtin_nontemporal_store((uint32_t)v, (uint32_t*)p);
+  else __builtin_nontemporal_store(v, (uint64_t*)p);
+}
+
+template <int W>
 struct WidthTag {
   static constexpr int value = W;
 };
@@ -698,7 +706,11 @@ __global__ __launch_bounds__(kMaxBins) void tile_offs_kernel(
 // store would wait for it). HBM then always has a tile's worth of loads in
 // flight per workgroup, and neighbouring tiles' runs into one bucket are
 // written by one workgroup (their partial lines meet in one L2).
+#if SRS_SCATTER_NT
+#define SCATTER_STORE stw_nt
+#else
 #define SCATTER_STORE stw
+#endif
 #if SRS_DEBUG_SEQ_WRITE  // timing experiment only: every tile written in place, unsorted order
 #define SCATTER_DST(d) (ti.base)
 #else
