@@ -98,9 +98,6 @@ struct ListCounters {
 #ifndef SRS_SCATTER_WG_PER_CU
 #define SRS_SCATTER_WG_PER_CU 2
 #endif
-#ifndef SRS_LOCAL_PREFETCH
-#define SRS_LOCAL_PREFETCH 0
-#endif
 #ifndef SRS_LOCAL_RANK_SPLIT
 #define SRS_LOCAL_RANK_SPLIT 2
 #endif

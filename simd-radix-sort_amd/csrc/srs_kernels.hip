@@ -1076,22 +1076,6 @@ with_width(w, [&](auto W_) {
   }
 });
   }
-#if SRS_LOCAL_PREFETCH
-  // the first payload column is loaded with the keys: its latency then
-  // overlaps the sort instead of following it
-  uint64_t v1[IT];
-  if (ncols > 1) {
-    const char* src = desc->cols[1].base[g.buf];
-    const uint32_t w = desc->cols[1].width, st = desc->cols[1].stride;
-with_width(w, [&](auto W_) {
-#pragma unroll
-  for (int k = 0; k < IT; k++) {
-    const int e = ebase + k * 64;
-    v1[k] = e < cnt ? ldw<decltype(W_)::value>(src + (base + e) * (int64_t)st) : 0;
-  }
-});
-  }
-#endif
   const U uref = xf((U)(load_w(desc->cols[0].base[g.buf] + base * (int64_t)desc->cols[0].stride,
                                desc->cols[0].width) & kmask));
   // keys are recomputed from v0 when needed (holding them costs occupancy)
@@ -1218,42 +1202,42 @@ with_width(w, [&](auto W_) {
   for (int k = 0; k < IT; k++) id[k] = perm[ebase + k * 64];
 
   // ---- 4. columns: stage in input order, write in output order --------------
-  // (in place is safe: every load of a column completes before the barrier
-  // that precedes its stores)
-  for (int c = 0; c < ncols; c++) {
+  // Software-pipelined: column c+1's loads are issued before column c is
+  // staged and stored, so their latency hides behind that work. In place is
+  // safe: a column's loads complete before the barrier that precedes its own
+  // stores, and different columns never share bytes.
+  auto load_col = [&](int c, uint64_t (&dst)[IT]) {
     const char* src = desc->cols[c].base[g.buf];
+    const uint32_t st = desc->cols[c].stride;
+    with_width(desc->cols[c].width, [&](auto W_) {
+#pragma unroll
+      for (int k = 0; k < IT; k++) {
+        const int e = ebase + k * 64;
+        dst[k] = e < cnt ? ldw<decltype(W_)::value>(src + (base + e) * (int64_t)st) : 0;
+      }
+    });
+  };
+  uint64_t vn[IT];
+  if (ncols > 1) load_col(1, vn);
+  for (int c = 0; c < ncols; c++) {
     char* out = desc->cols[c].base[BUF_OUT];
-    const uint32_t w = desc->cols[c].width, st = desc->cols[c].stride;
+    const uint32_t st = desc->cols[c].stride;
     uint64_t v[IT];
-    if (c == 0) {
 #pragma unroll
-      for (int k = 0; k < IT; k++) v[k] = v0[k];
-#if SRS_LOCAL_PREFETCH
-    } else if (c == 1) {
-#pragma unroll
-      for (int k = 0; k < IT; k++) v[k] = v1[k];
-#endif
-    } else {
-with_width(w, [&](auto W_) {
-#pragma unroll
-  for (int k = 0; k < IT; k++) {
-    const int e = ebase + k * 64;
-    v[k] = e < cnt ? ldw<decltype(W_)::value>(src + (base + e) * (int64_t)st) : 0;
-  }
-});
-    }
+    for (int k = 0; k < IT; k++) v[k] = c == 0 ? v0[k] : vn[k];
+    if (c >= 1 && c + 1 < ncols) load_col(c + 1, vn);
     lds_barrier();  // previous users of sbuf are done
 #pragma unroll
     for (int k = 0; k < IT; k++)
       if (valid(k)) sbuf[ebase + k * 64] = v[k];
     lds_barrier();
-with_width(w, [&](auto W_) {
+    with_width(desc->cols[c].width, [&](auto W_) {
 #pragma unroll
-  for (int k = 0; k < IT; k++) {
-    const int e = ebase + k * 64;
-    if (valid(k)) stw<decltype(W_)::value>(out + (base + e) * (int64_t)st, sbuf[id[k]]);
-  }
-});
+      for (int k = 0; k < IT; k++) {
+        const int e = ebase + k * 64;
+        if (valid(k)) stw<decltype(W_)::value>(out + (base + e) * (int64_t)st, sbuf[id[k]]);
+      }
+    });
     STAMP();  // 5, 6: column moved
   }
   STAMP_FLUSH(1);
@@ -1468,38 +1452,43 @@ with_width(w, [&](auto W_) {
 #pragma unroll
   for (int k = 0; k < IT; k++) id[k] = perm[ebase + k * 64];
 
-  // ---- 5. columns: stage in input order, write in output order --------------
-  // (in place is safe: every load of a column completes before the barrier
-  // that precedes its stores)
-  for (int c = 0; c < ncols; c++) {
+  // ---- 5. columns, software-pipelined as in local_kernel -------------------
+  auto load_col = [&](int c, uint64_t (&dst)[IT]) {
     const char* src = desc->cols[c].base[g.buf];
-    char* out = desc->cols[c].base[BUF_OUT];
-    const uint32_t w = desc->cols[c].width, st = desc->cols[c].stride;
-    uint64_t v[IT];
-    if (SRS_LOCAL_KEEP_KEYS && c == 0) {
+    const uint32_t st = desc->cols[c].stride;
+    with_width(desc->cols[c].width, [&](auto W_) {
 #pragma unroll
-      for (int k = 0; k < IT; k++) v[k] = v0[k];
-    } else {
-with_width(w, [&](auto W_) {
-#pragma unroll
-  for (int k = 0; k < IT; k++) {
-    const int e = ebase + k * 64;
-    v[k] = e < cnt ? ldw<decltype(W_)::value>(src + (base + e) * (int64_t)st) : 0;
+      for (int k = 0; k < IT; k++) {
+        const int e = ebase + k * 64;
+        dst[k] = e < cnt ? ldw<decltype(W_)::value>(src + (base + e) * (int64_t)st) : 0;
+      }
+    });
+  };
+  uint64_t vn[IT];
+  if (SRS_LOCAL_KEEP_KEYS) {
+    if (ncols > 1) load_col(1, vn);
+  } else {
+    load_col(0, vn);
   }
-});
-    }
+  for (int c = 0; c < ncols; c++) {
+    char* out = desc->cols[c].base[BUF_OUT];
+    const uint32_t st = desc->cols[c].stride;
+    uint64_t v[IT];
+#pragma unroll
+    for (int k = 0; k < IT; k++) v[k] = (SRS_LOCAL_KEEP_KEYS && c == 0) ? v0[k] : vn[k];
+    if ((!SRS_LOCAL_KEEP_KEYS || c >= 1) && c + 1 < ncols) load_col(c + 1, vn);
     lds_barrier();  // previous users of sbuf are done
 #pragma unroll
     for (int k = 0; k < IT; k++)
       if (valid(k)) sbuf[ebase + k * 64] = v[k];
     lds_barrier();
-with_width(w, [&](auto W_) {
+    with_width(desc->cols[c].width, [&](auto W_) {
 #pragma unroll
-  for (int k = 0; k < IT; k++) {
-    const int e = ebase + k * 64;
-    if (valid(k)) stw<decltype(W_)::value>(out + (base + e) * (int64_t)st, sbuf[id[k]]);
-  }
-});
+      for (int k = 0; k < IT; k++) {
+        const int e = ebase + k * 64;
+        if (valid(k)) stw<decltype(W_)::value>(out + (base + e) * (int64_t)st, sbuf[id[k]]);
+      }
+    });
   }
   }
 }
