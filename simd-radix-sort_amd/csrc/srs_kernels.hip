@@ -1044,6 +1044,12 @@ __global__ __launch_bounds__(NT, WPE) void local_kernel(const SortDesc* __restri
   __shared__ int maxlen;
 
   const Seg g = segs[blockIdx.x];
+  if (g.rbits <= kLocalTopBits) {
+    // the stable kernel's single ballot pass resolves every remaining bit
+    // (and duplicate-heavy data would overflow the rank step here anyway)
+    if (threadIdx.x == 0) fallback[atomicAdd(fallback_count, 1ull)] = g;
+    return;
+  }
   const uint32_t wave = threadIdx.x >> 6;
   const uint32_t lane = lane_id();
   const int ebase = (int)wave * IT * 64 + (int)lane;  // element of slot k: ebase + 64 k

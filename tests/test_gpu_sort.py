@@ -364,3 +364,69 @@ def test_sort_segments_device(kind):
         exp_k[a:b] = keys_h[a:b][o]
         exp_p[a:b] = pay_h[a:b][o]
     assert bytes_equal(ko, exp_k) and np.array_equal(po, exp_p)
+
+
+# ---------------------------------------------------------------------------
+# scale: adversarial distributions at 5e7 against torch's stable sort, and
+# more than 2^32 keys (64-bit positions everywhere)
+# ---------------------------------------------------------------------------
+def _device_keys(torch, dist, n, g):
+    i64 = torch.int64
+    if dist == "uniform":
+        return torch.randint(-2**63, 2**63 - 1, (n,), dtype=i64, device="cuda", generator=g)
+    if dist == "equal":
+        return torch.full((n,), 12345, dtype=i64, device="cuda")
+    if dist == "zeroone":
+        return torch.randint(0, 2, (n,), dtype=i64, device="cuda", generator=g)
+    if dist == "fewdistinct":
+        vals = torch.randint(-2**63, 2**63 - 1, (37,), dtype=i64, device="cuda", generator=g)
+        return vals[torch.randint(0, 37, (n,), device="cuda", generator=g)]
+    if dist == "dup64":  # every value ~64 times (duplicate-heavy local segments)
+        return torch.randint(0, n // 64, (n,), dtype=i64, device="cuda", generator=g) * 7919
+    if dist == "sorted":
+        return torch.sort(torch.randint(0, 2**62, (n,), dtype=i64, device="cuda", generator=g))[0]
+    if dist == "reverse":
+        return torch.sort(torch.randint(0, 2**62, (n,), dtype=i64, device="cuda",
+                                        generator=g))[0].flip(0)
+    if dist == "highbits":
+        return torch.randint(0, 256, (n,), dtype=i64, device="cuda", generator=g) << 56
+    if dist == "lowbits":
+        return torch.randint(0, 256, (n,), dtype=i64, device="cuda", generator=g)
+    if dist == "gaussian":
+        return (torch.randn(n, device="cuda", generator=g) * 1e6).round().to(i64)
+    raise ValueError(dist)
+
+
+@pytest.mark.parametrize("dist", ["uniform", "equal", "zeroone", "fewdistinct", "dup64",
+                                  "sorted", "reverse", "highbits", "lowbits", "gaussian"])
+def test_scale_distributions_vs_torch_stable(dist):
+    """5e7 u64 keys + their input index as payload: keys and payloads must
+    equal torch's stable sort (signed view of the unsigned order) exactly."""
+    torch = _torch()
+    n = 50_000_017
+    g = torch.Generator(device="cuda")
+    g.manual_seed(11)
+    keys = _device_keys(torch, dist, n, g)
+    pay = torch.arange(n, dtype=torch.int64, device="cuda")
+    ko, po = torch.empty_like(keys), torch.empty_like(pay)
+    srs_amd.sort_device(keys, pay, key_kind=srs_amd.KEY_U64, out=(ko, po))
+    ref_k, ref_i = torch.sort(keys ^ torch.iinfo(torch.int64).min, stable=True)
+    assert torch.equal(ko, ref_k ^ torch.iinfo(torch.int64).min)
+    assert torch.equal(po, ref_i)
+
+
+def test_more_than_2_pow_32_keys():
+    """n > 2^32: positions, tile indices and offsets are 64-bit throughout.
+    u32 keys (17 GB), in place; checked by order and by two multiset sums."""
+    torch = _torch()
+    n = (1 << 32) + 1027
+    g = torch.Generator(device="cuda")
+    g.manual_seed(3)
+    keys = torch.randint(-2**31, 2**31 - 1, (n,), dtype=torch.int32, device="cuda", generator=g)
+    wide = keys.to(torch.int64) & 0xFFFFFFFF
+    s1, s2 = int(wide.sum().item()), int((wide * wide).sum().item())
+    del wide
+    srs_amd.sort_device(keys, key_kind=srs_amd.KEY_U32)
+    wide = keys.to(torch.int64) & 0xFFFFFFFF
+    assert bool((wide[1:] >= wide[:-1]).all().item())
+    assert int(wide.sum().item()) == s1 and int((wide * wide).sum().item()) == s2
