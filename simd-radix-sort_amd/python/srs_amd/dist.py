@@ -186,8 +186,9 @@ class ShardSorter:
         rk = self.recv_keys[:total]
         rps = [b[:total] for b in self.recv_pays]
         cols = [(self.part_keys, rk)] + list(zip(self.part_pays, rps))
-        # 6: rounds of peer-to-peer moves; sort each round's groups meanwhile
-        for r in range(R):
+        # 6: rounds of peer-to-peer moves; round r+1 is in flight before the
+        # (host-synchronising) sort of round r's groups is queued
+        def issue(r):
             p2p = []
             for g in range(G):
                 if rnd[g] != r:
@@ -207,9 +208,13 @@ class ShardSorter:
                 elif counts[g]:
                     for sbuf, _ in cols:
                         self._msgs(p2p, dist.isend, sbuf, soff[g], counts[g], dst)
-            if p2p:
-                for req in dist.batch_isend_irecv(p2p):
-                    req.wait()
+            return dist.batch_isend_irecv(p2p) if p2p else []
+
+        pending = issue(0)
+        for r in range(R):
+            for req in pending:
+                req.wait()
+            pending = issue(r + 1) if r + 1 < R else []
             mine = [g for g in owned[me] if rnd[g] == r]
             if mine:
                 bounds = [gbound[mine[0]][0]] + [gbound[g][1] for g in mine]
