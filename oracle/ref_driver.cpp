@@ -14,6 +14,7 @@
 // pack) needs an instantiation; payload types only matter through their
 // sizes, so payloads are instantiated as unsigned integers of the given
 // size, and DataElement payload bytes as one std::array<uint8_t, N>.
+#include <time.h>
 #include <array>
 #include <cstdint>
 #include <cstring>
@@ -140,6 +141,20 @@ int srs_ref_sort_aos(int64_t num, int kind, int up, int64_t thresh, void* elems,
 #define CALL(K, U) sort_aos_k<K, U>(thresh, num, elems, esz)
   SRS_KIND_SWITCH(CALL)
 #undef CALL
+}
+
+// srs_ref_sort_soa timed the way the reference's perf harness times it
+// (src/perf.hpp:33-46): CLOCK_PROCESS_CPUTIME_ID around the sort call only;
+// the elapsed nanoseconds go to *cpu_ns.
+int srs_ref_sort_soa_timed(int64_t num, int kind, int up, int64_t thresh, void* keys,
+                           int32_t np, void* const* pays, const uint32_t* sz,
+                           double* cpu_ns) {
+  struct timespec a, b;
+  clock_gettime(CLOCK_PROCESS_CPUTIME_ID, &a);
+  const int rc = srs_ref_sort_soa(num, kind, up, thresh, keys, np, pays, sz);
+  clock_gettime(CLOCK_PROCESS_CPUTIME_ID, &b);
+  if (cpu_ns) *cpu_ns = (b.tv_sec - a.tv_sec) * 1e9 + (double)(b.tv_nsec - a.tv_nsec);
+  return rc;
 }
 
 const char* srs_ref_build_info(void) {
