@@ -182,6 +182,7 @@ struct Workspace {
   DevBuf big[2], local, local2, copy, fallback, fallback2;
   DevBuf plan, tcount, gcount, tbase, gbase, var, sbase;
   DevBuf tile_seg, group_seg, hist, offs, gsum, gofs, scan_tmp, totals, ctr;
+  DevBuf shist, lut, lut_rbits;  // balanced first level (sampled histogram, digit table)
   ListCounters* h_ctr = nullptr;
   uint64_t* h_totals = nullptr;
 };
@@ -254,6 +255,70 @@ void key_masks(int kind, int up, SortDesc& d) {
   d.key_bits = kb;
 }
 
+// ---- balanced first level ---------------------------------------------------
+// A plain first digit (the top bits) is fine for uniform keys but wastes a
+// level on skewed ones: uniform floats in [-1, 1) put a quarter of all keys
+// under one exponent, so three levels are needed instead of two. For large
+// inputs a sampled 16-bit histogram (a few million keys in contiguous chunks)
+// decides; if some top-9-bit bucket would hold more than kSkew times its
+// share, the first level instead sends the keys to 512 key-range groups of
+// ~equal size through a 16-bit digit table (the multi-GPU partition's LUT
+// digit). Each group's children start below the key prefix its bins share.
+constexpr int64_t kBalancedMinN = int64_t(1) << 24;
+constexpr int kBalancedSkew = 4;
+constexpr int kGroups = kMaxBins;
+
+int plan_balanced_level(Workspace* W, const Request& R, const SortDesc& d, bool* use,
+                        hipStream_t st) {
+  *use = false;
+  const int ks = key_size_of(R.kind);
+  const int64_t n = R.num;
+  if (R.nsegs > 0 || R.aos || n < kBalancedMinN || ks < 4) return SRS_OK;
+  constexpr int kChunk = 1024;
+  const int64_t blocks = std::min<int64_t>(4096, n / kChunk);
+  const int64_t stride = n / blocks;
+  SRS_TRY(ensure(W->shist, 65536 * sizeof(uint32_t)));
+  HIP_TRY(hipMemsetAsync(W->shist.p, 0, 65536 * sizeof(uint32_t), st));
+  launch_sample_hist16(R.in_cols[0], ks, n, stride, kChunk, blocks, d.mpos, d.mneg,
+                       (uint32_t*)W->shist.p, st);
+  std::vector<uint32_t> h(65536);
+  HIP_TRY(hipMemcpyAsync(h.data(), W->shist.p, h.size() * 4, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  uint64_t total = 0, top9max = 0;
+  for (int b = 0; b < 512; b++) {
+    uint64_t t = 0;
+    for (int j = 0; j < 128; j++) t += h[b * 128 + j];
+    total += t;
+    top9max = std::max(top9max, t);
+  }
+  if (total == 0 || top9max * 512 <= (uint64_t)kBalancedSkew * total) return SRS_OK;
+  // bins -> groups: group of bin b = floor(G * (keys before b + half of b) / total)
+  std::vector<int32_t> lut(65536), first(kGroups, -1), last(kGroups, -1), rbits(kGroups);
+  double before = 0;
+  for (int b = 0; b < 65536; b++) {
+    int g = (int)((before + 0.5 * h[b]) * kGroups / (double)total);
+    g = std::min(std::max(g, b ? lut[b - 1] : 0), kGroups - 1);
+    lut[b] = g;
+    if (first[g] < 0) first[g] = b;
+    last[g] = b;
+    before += h[b];
+  }
+  for (int g = 0; g < kGroups; g++) {
+    const int diff = first[g] < 0 ? 0xFFFF : (first[g] ^ last[g]);
+    int bl = 0;
+    while ((1 << bl) <= diff) bl++;
+    rbits[g] = d.key_bits - (16 - bl);  // the group's keys share 16 - bl top bits
+  }
+  SRS_TRY(ensure(W->lut, 65536 * sizeof(int32_t)));
+  SRS_TRY(ensure(W->lut_rbits, kGroups * sizeof(int32_t)));
+  HIP_TRY(hipMemcpyAsync(W->lut.p, lut.data(), lut.size() * 4, hipMemcpyHostToDevice, st));
+  HIP_TRY(hipMemcpyAsync(W->lut_rbits.p, rbits.data(), rbits.size() * 4, hipMemcpyHostToDevice,
+                         st));
+  HIP_TRY(hipStreamSynchronize(st));  // the host vectors go out of scope
+  *use = true;
+  return SRS_OK;
+}
+
 struct LevelState {
   int64_t nbig, n_local, n_local2, n_copy;
   int cur;
@@ -264,7 +329,7 @@ struct LevelState {
 // W->big[S.cur ^ 1] / the local lists / the copy list; S is updated from the
 // device counters. force_bits / lut: partition passes (srs_partition_device).
 int run_level(Workspace* W, int ks, const SortDesc* d_desc, LevelState& S, int force_bits,
-              bool lut, hipStream_t st) {
+              bool lut, hipStream_t st, const int32_t* lut_rbits = nullptr) {
   const int64_t nbig = S.nbig;
   ListCounters* d_ctr = (ListCounters*)W->ctr.p;
   uint64_t* d_totals = (uint64_t*)W->totals.p;
@@ -326,7 +391,7 @@ int run_level(Workspace* W, int ks, const SortDesc* d_desc, LevelState& S, int f
     launch_offsets(plan, nbig, group_seg, ngroups, (uint32_t*)W->hist.p,
                    (uint32_t*)W->gsum.p, (uint64_t*)W->gofs.p, (uint64_t*)W->sbase.p,
                    (uint64_t*)W->offs.p, var, (Seg*)W->big[nxt].p, (Seg*)W->local.p,
-                   (Seg*)W->local2.p, (Seg*)W->copy.p, d_ctr, st);
+                   (Seg*)W->local2.p, (Seg*)W->copy.p, d_ctr, lut_rbits, st);
   }
   {
     TimedScope ts("scatter", (double)0, st);
@@ -392,6 +457,13 @@ int run_sort(Workspace* W, const Request& R, hipStream_t st) {
     for (int c = 0; c < d.ncols; c++) d.cols[c].base[BUF_IN] = d.cols[c].base[BUF_OUT];
 
   d.stamp_acc = g_stamp_acc;
+  bool balanced = false;
+  SRS_TRY(plan_balanced_level(W, R, d, &balanced, st));
+  if (balanced) {
+    d.digit_lut = (const int32_t*)W->lut.p;
+    d.lut_shift = d.key_bits - 16;
+    d.lut_bits = 16;
+  }
   SRS_TRY(ensure(W->desc, sizeof(SortDesc)));
   SortDesc* d_desc = (SortDesc*)W->desc.p;
   launch_set_desc(d, d_desc, st);
@@ -459,6 +531,11 @@ int run_sort(Workspace* W, const Request& R, hipStream_t st) {
   }
   LevelState S{n_big, n_local, n_local2, n_copy, 0};
   int level = 0;
+  if (balanced && S.nbig > 0) {
+    ++level;
+    SRS_TRY(run_level(W, ks, d_desc, S, kMaxDigitBits, true, st,
+                      (const int32_t*)W->lut_rbits.p));
+  }
   while (S.nbig > 0) {
     if (++level > 80) return fail(SRS_ERR_INTERNAL, "level limit exceeded");
     SRS_TRY(run_level(W, ks, d_desc, S, 0, false, st));
@@ -893,7 +970,7 @@ int srs_release_workspace(void) {
   std::lock_guard<std::mutex> lk(g_wmu);
   for (auto& kv : g_ws) {
     Workspace* w = kv.second;
-    DevBuf* bufs[] = {&w->tmp, &w->stage, &w->desc, &w->big[0], &w->big[1], &w->local, &w->local2, &w->fallback, &w->fallback2,
+    DevBuf* bufs[] = {&w->tmp, &w->stage, &w->desc, &w->big[0], &w->big[1], &w->local, &w->local2, &w->fallback, &w->fallback2, &w->shist, &w->lut, &w->lut_rbits,
                       &w->copy, &w->plan, &w->tcount, &w->gcount, &w->tbase, &w->gbase,
                       &w->var, &w->sbase, &w->tile_seg, &w->group_seg, &w->hist, &w->offs,
                       &w->gsum, &w->gofs, &w->scan_tmp, &w->totals, &w->ctr};

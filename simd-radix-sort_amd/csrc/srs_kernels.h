@@ -24,7 +24,8 @@ void launch_excl_scan(const uint64_t* x, uint64_t* y, int64_t n, uint64_t* temp,
 void launch_offsets(SegPlan* plan, int64_t nbig, const int32_t* group_seg, int64_t ngroups,
                     const uint32_t* hist, uint32_t* gsum, uint64_t* gofs, uint64_t* sbase,
                     uint64_t* offs, const unsigned long long* var_or, Seg* big_next,
-                    Seg* local, Seg* local2, Seg* copy, ListCounters* ctr, hipStream_t st);
+                    Seg* local, Seg* local2, Seg* copy, ListCounters* ctr,
+                    const int32_t* lut_rbits, hipStream_t st);
 void launch_scatter(int key_size, const SortDesc* d, const SegPlan* plan,
                     const int32_t* tile_seg, const uint64_t* offs, int64_t ntiles, bool lut,
                     hipStream_t st);
@@ -37,6 +38,9 @@ void launch_local_stable(int key_size, const SortDesc* d, const Seg* segs,
                          unsigned long long* fallback_count, int grid, hipStream_t st);
 void launch_local_lsd(int key_size, const SortDesc* d, const Seg* segs,
                       const unsigned long long* nsegs, int grid, hipStream_t st);
+void launch_sample_hist16(const void* keys, int key_bytes, int64_t n, int64_t stride, int chunk,
+                          int64_t blocks, uint64_t mpos, uint64_t mneg, uint32_t* hist,
+                          hipStream_t st);
 void launch_fill(int64_t n, int kind, uint64_t seed, uint64_t first, void* keys,
                  int npay, const Col* pays, hipStream_t st);
 void launch_set_desc(const SortDesc& d, SortDesc* out, hipStream_t st);

@@ -325,7 +325,7 @@ __global__ void plan_kernel(const Seg* __restrict__ big, int64_t nbig,
   p.start = g.start;
   p.len = g.len;
   p.bits = force_bits ? force_bits : choose_bits(g.len, g.rbits);
-  p.shift = force_bits ? 0 : g.rbits - p.bits;
+  p.shift = force_bits ? g.rbits : g.rbits - p.bits;  // LUT levels consume no fixed bits
   p.ntiles = (int32_t)((g.len + kTile - 1) / kTile);
   p.ngroups = (p.ntiles + kScanGroup - 1) / kScanGroup;
   p.buf = g.buf;
@@ -611,7 +611,7 @@ __global__ __launch_bounds__(kMaxBins) void seg_scan_kernel(
     SegPlan* __restrict__ plan, const uint32_t* __restrict__ gsum,
     uint64_t* __restrict__ gofs, uint64_t* __restrict__ sbase,
     const unsigned long long* __restrict__ var_or, Seg* big_next, Seg* local, Seg* local2,
-    Seg* copy, ListCounters* ctr) {
+    Seg* copy, ListCounters* ctr, const int32_t* __restrict__ lut_rbits) {
   __shared__ uint64_t scan_sh[kMaxBins / 64 + 1];
   __shared__ int single;
   const int64_t s = blockIdx.x;
@@ -657,7 +657,8 @@ __global__ __launch_bounds__(kMaxBins) void seg_scan_kernel(
   } else if (b < nb && run > 0) {
     c.start = P.start + (int64_t)ex;
     c.len = (int64_t)run;
-    c.rbits = P.shift;
+    // a LUT level's group b is a key range whose keys share a known prefix
+    c.rbits = (lut_rbits && lut_rbits[b] < P.shift) ? lut_rbits[b] : P.shift;
     c.buf = P.dst;
   }
   emit_children_block(Lists{big_next, local, local2, copy, ctr}, c);
@@ -1601,6 +1602,30 @@ __global__ __launch_bounds__(kLocalStableThreads) void local_lsd_kernel(
 }
 
 // ---------------------------------------------------------------------------
+// sampled 16-bit key histogram (balanced first level): block b
+// counts the transformed top 16 bits of keys [b*stride, b*stride + chunk)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void sample_hist16_kernel(
+    const char* __restrict__ keys, int key_bytes, int64_t n, int64_t stride, int chunk,
+    uint64_t mpos, uint64_t mneg, uint32_t* __restrict__ hist) {
+  const int kb = 8 * key_bytes;
+  const int64_t a = (int64_t)blockIdx.x * stride;
+  const int64_t e = min(n, a + chunk);
+  for (int64_t i = a + threadIdx.x; i < e; i += 256) {
+    const uint64_t bits = load_w(keys + i * key_bytes, key_bytes);
+    const uint64_t u = bits ^ (((bits >> (kb - 1)) & 1) ? mneg : mpos);
+    atomicAdd(&hist[(uint32_t)(u >> (kb - 16)) & 0xFFFF], 1u);
+  }
+}
+
+void launch_sample_hist16(const void* keys, int key_bytes, int64_t n, int64_t stride, int chunk,
+                          int64_t blocks, uint64_t mpos, uint64_t mneg, uint32_t* hist,
+                          hipStream_t st) {
+  sample_hist16_kernel<<<(unsigned)blocks, 256, 0, st>>>((const char*)keys, key_bytes, n, stride,
+                                                         chunk, mpos, mneg, hist);
+}
+
+// ---------------------------------------------------------------------------
 // synthetic data (bench / tests): splitmix64 of the global index
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
@@ -1697,10 +1722,12 @@ void launch_excl_scan(const uint64_t* x, uint64_t* y, int64_t n, uint64_t* temp,
 void launch_offsets(SegPlan* plan, int64_t nbig, const int32_t* group_seg, int64_t ngroups,
                     const uint32_t* hist, uint32_t* gsum, uint64_t* gofs, uint64_t* sbase,
                     uint64_t* offs, const unsigned long long* var_or, Seg* big_next,
-                    Seg* local, Seg* local2, Seg* copy, ListCounters* ctr, hipStream_t st) {
+                    Seg* local, Seg* local2, Seg* copy, ListCounters* ctr,
+                    const int32_t* lut_rbits, hipStream_t st) {
   group_sum_kernel<<<(unsigned)ngroups, kMaxBins, 0, st>>>(plan, group_seg, hist, gsum);
   seg_scan_kernel<<<(unsigned)nbig, kMaxBins, 0, st>>>(plan, gsum, gofs, sbase, var_or,
-                                                      big_next, local, local2, copy, ctr);
+                                                      big_next, local, local2, copy, ctr,
+                                                      lut_rbits);
   tile_offs_kernel<<<(unsigned)ngroups, kMaxBins, 0, st>>>(plan, group_seg, hist, gofs, sbase,
                                                           offs);
 }

@@ -430,3 +430,33 @@ def test_more_than_2_pow_32_keys():
     wide = keys.to(torch.int64) & 0xFFFFFFFF
     assert bool((wide[1:] >= wide[:-1]).all().item())
     assert int(wide.sum().item()) == s1 and int((wide * wide).sum().item()) == s2
+
+
+@pytest.mark.parametrize("dist", ["f32grid", "f32normal", "f64normal", "f64uniform"])
+def test_scale_float_keys_vs_torch_stable(dist):
+    """5e7 float keys (C2's grid distribution included: heavy duplicates and
+    a quarter of the keys under one exponent -> the balanced first level) +
+    input index payload, against torch's stable sort (no -0.0 and no NaN in
+    the inputs, so float order equals the reference's bit order)."""
+    torch = _torch()
+    n = 50_000_021
+    g = torch.Generator(device="cuda")
+    g.manual_seed(5)
+    if dist == "f32grid":
+        keys = (torch.randint(0, 1 << 24, (n,), device="cuda", generator=g).to(torch.float32)
+                * (1.0 / (1 << 23)) - 1.0)
+    elif dist == "f32normal":
+        keys = torch.randn(n, device="cuda", generator=g)
+    elif dist == "f64normal":
+        keys = torch.randn(n, device="cuda", generator=g, dtype=torch.float64)
+    else:
+        keys = torch.rand(n, device="cuda", generator=g, dtype=torch.float64) * 2 - 1
+    keys = torch.where(keys == 0, torch.zeros_like(keys), keys)  # no -0.0
+    kind = srs_amd.KEY_F32 if keys.dtype == torch.float32 else srs_amd.KEY_F64
+    pay = torch.arange(n, dtype=torch.int64, device="cuda")
+    ko, po = torch.empty_like(keys), torch.empty_like(pay)
+    srs_amd.sort_device(keys, pay, key_kind=kind, out=(ko, po))
+    ref_k, ref_i = torch.sort(keys, stable=True)
+    assert torch.equal(ko.view(torch.int32 if kind == srs_amd.KEY_F32 else torch.int64),
+                       ref_k.view(torch.int32 if kind == srs_amd.KEY_F32 else torch.int64))
+    assert torch.equal(po, ref_i)
