@@ -269,7 +269,7 @@ constexpr int kBalancedSkew = 4;
 constexpr int kGroups = kMaxBins;
 
 int plan_balanced_level(Workspace* W, const Request& R, const SortDesc& d, bool* use,
-                        hipStream_t st) {
+                        int* lut_entries, hipStream_t st) {
   *use = false;
   const int ks = key_size_of(R.kind);
   const int64_t n = R.num;
@@ -309,9 +309,25 @@ int plan_balanced_level(Workspace* W, const Request& R, const SortDesc& d, bool*
     while ((1 << bl) <= diff) bl++;
     rbits[g] = d.key_bits - (16 - bl);  // the group's keys share 16 - bl top bits
   }
-  SRS_TRY(ensure(W->lut, 65536 * sizeof(int32_t)));
+  // two-level u16 table (DigitLut mode 1): a 12-bit bin whose 16 sub-bins
+  // fall into one group maps straight to it; a split bin points to 16 entries
+  std::vector<uint16_t> t2(4096);
+  for (int B = 0; B < 4096; B++) {
+    bool same = true;
+    for (int j = 1; j < 16; j++) same &= lut[B * 16 + j] == lut[B * 16];
+    if (same) {
+      t2[B] = (uint16_t)lut[B * 16];
+    } else {
+      const int idx = (int)(t2.size() - 4096) / 16;
+      t2[B] = (uint16_t)(0x8000 | idx);
+      for (int j = 0; j < 16; j++) t2.push_back((uint16_t)lut[B * 16 + j]);
+    }
+  }
+  if ((int)t2.size() > kLdsLutEntries) return fail(SRS_ERR_INTERNAL, "digit table too large");
+  *lut_entries = (int)t2.size();
+  SRS_TRY(ensure(W->lut, t2.size() * sizeof(uint16_t)));
   SRS_TRY(ensure(W->lut_rbits, kGroups * sizeof(int32_t)));
-  HIP_TRY(hipMemcpyAsync(W->lut.p, lut.data(), lut.size() * 4, hipMemcpyHostToDevice, st));
+  HIP_TRY(hipMemcpyAsync(W->lut.p, t2.data(), t2.size() * 2, hipMemcpyHostToDevice, st));
   HIP_TRY(hipMemcpyAsync(W->lut_rbits.p, rbits.data(), rbits.size() * 4, hipMemcpyHostToDevice,
                          st));
   HIP_TRY(hipStreamSynchronize(st));  // the host vectors go out of scope
@@ -458,11 +474,14 @@ int run_sort(Workspace* W, const Request& R, hipStream_t st) {
 
   d.stamp_acc = g_stamp_acc;
   bool balanced = false;
-  SRS_TRY(plan_balanced_level(W, R, d, &balanced, st));
+  int lut_entries = 0;
+  SRS_TRY(plan_balanced_level(W, R, d, &balanced, &lut_entries, st));
   if (balanced) {
     d.digit_lut = (const int32_t*)W->lut.p;
     d.lut_shift = d.key_bits - 16;
     d.lut_bits = 16;
+    d.lut_mode = 1;
+    d.lut_entries = lut_entries;
   }
   SRS_TRY(ensure(W->desc, sizeof(SortDesc)));
   SortDesc* d_desc = (SortDesc*)W->desc.p;

@@ -43,7 +43,9 @@ struct SortDesc {
   // partition passes only: digit = digit_lut[u >> lut_shift]
   const int32_t* digit_lut;
   int32_t lut_shift;
-  int32_t lut_bits;   // table size 2^lut_bits; staged in LDS when <= kLdsLutBits
+  int32_t lut_bits;   // mode 0: table size 2^lut_bits; staged in LDS when <= kLdsLutBits
+  int32_t lut_mode;   // 0 flat int32 table, 1 two-level u16 table (see DigitLut)
+  int32_t lut_entries;  // mode 1: u16 entries (4096 + 16 per split bin)
   unsigned long long* stamp_acc;  // diagnostic builds only (SRS_STAMPS)
 };
 
@@ -118,7 +120,8 @@ constexpr int kMaxBins = 1 << kMaxDigitBits;   // histogram row stride (tile-maj
 static_assert(kScatterThreads >= kMaxBins, "the scatter tile scan gives one bin per thread");
 constexpr int kScanGroup = 256;                 // tiles per column-scan group
 constexpr int kHistMaxBits = 12;                // srs_key_histogram_device
-constexpr int kLdsLutBits = 12;                 // digit tables up to 16 KB live in LDS
+constexpr int kLdsLutBits = 12;                 // flat digit tables up to 4096 entries live in LDS
+constexpr int kLdsLutEntries = 4096 + 16 * 512; // two-level table worst case (24 KB of u16)
 
 // local sort classes: fast kernel (atomic bucket pass + rank) in two sizes,
 // then the stable kernel and the LSD kernel as fallbacks (same capacity as

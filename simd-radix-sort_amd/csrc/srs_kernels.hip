@@ -110,14 +110,32 @@ struct Xform {
 
 __device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63; }
 
+// Digit table of a LUT pass (partition / balanced first level). Tables are
+// read from LDS (u16 entries) when they fit, from global memory otherwise.
+//   mode 0: flat, entry [u >> shift] (2^lut_bits entries)
+//   mode 1: two-level: entry t = [u >> (shift + 4)] of a 4096-entry table;
+//           if t has bit 15 set, the group is [4096 + (t & 0x7fff) * 16 +
+//           ((u >> shift) & 15)] (a 12-bit bin split between groups).
+struct DigitLut {
+  const uint16_t* s;  // LDS copy, or null
+  const int32_t* g;   // global flat table (mode 0 only, when s is null)
+  int shift;
+  int mode;
+};
+
 // Digit of a transformed key for a global pass: the key's bits
-// [shift, shift + bits), or (LUT) a group id looked up by its top bits (the
-// multi-GPU partition, whose groups are contiguous ranges of top-bit buckets).
+// [shift, shift + bits), or (LUT) a group id looked up by its top bits.
 template <bool LUT, typename U>
-__device__ __forceinline__ uint32_t pass_digit(U u, int shift, uint32_t mask, const int32_t* lut,
-                                               int lut_shift) {
-  if constexpr (LUT) return (uint32_t)lut[(uint64_t)u >> lut_shift];
-  else return (uint32_t)(u >> shift) & mask;
+__device__ __forceinline__ uint32_t pass_digit(U u, int shift, uint32_t mask, const DigitLut& L) {
+  if constexpr (LUT) {
+    const uint64_t x = (uint64_t)u >> L.shift;
+    if (L.mode == 1) {
+      const uint32_t t = L.s[x >> 4];
+      return (t & 0x8000u) ? L.s[4096 + ((t & 0x7fffu) << 4) + (uint32_t)(x & 15)] : t;
+    }
+    return L.s ? (uint32_t)L.s[x] : (uint32_t)L.g[x];
+  }
+  return (uint32_t)(u >> shift) & mask;
 }
 
 __device__ __forceinline__ uint32_t popc_below(uint64_t m) {
@@ -378,12 +396,24 @@ __device__ __forceinline__ int64_t xcd_remap(int64_t bid, int64_t nwg) {
 // Tables up to 2^kLdsLutBits entries are staged in LDS instead (the caller
 // barriers before the first use). Returns the table to read.
 template <bool LUT, int NT>
-__device__ __forceinline__ const int32_t* stage_lut(const SortDesc* desc, int32_t* slut) {
-  if (!LUT) return nullptr;
-  if (desc->lut_bits > kLdsLutBits) return desc->digit_lut;
-  const int n = 1 << desc->lut_bits;
-  for (int i = threadIdx.x; i < n; i += NT) slut[i] = desc->digit_lut[i];
-  return slut;
+__device__ __forceinline__ DigitLut stage_lut(const SortDesc* desc, uint16_t* slut) {
+  DigitLut L{nullptr, nullptr, 0, 0};
+  if (!LUT) return L;
+  L.shift = desc->lut_shift;
+  L.mode = desc->lut_mode;
+  if (L.mode == 1) {
+    const int n = desc->lut_entries;  // 4096 + 16 per split bin (<= kLdsLutEntries)
+    const uint16_t* src = (const uint16_t*)desc->digit_lut;
+    for (int i = threadIdx.x; i < n; i += NT) slut[i] = src[i];
+    L.s = slut;
+  } else if (desc->lut_bits <= kLdsLutBits) {
+    const int n = 1 << desc->lut_bits;
+    for (int i = threadIdx.x; i < n; i += NT) slut[i] = (uint16_t)desc->digit_lut[i];
+    L.s = slut;
+  } else {
+    L.g = desc->digit_lut;
+  }
+  return L;
 }
 
 // ---------------------------------------------------------------------------
@@ -406,9 +436,8 @@ __global__ __launch_bounds__(kCountThreads) void count_kernel(
   xf.init(*desc);
   const char* kp = desc->key.base[P.buf];
   const uint32_t ks = desc->key.stride;
-  __shared__ int32_t slut[LUT ? (1 << kLdsLutBits) : 1];
-  const int32_t* lut = stage_lut<LUT, kCountThreads>(desc, slut);
-  const int lut_shift = desc->lut_shift;
+  __shared__ uint16_t slut[LUT ? kLdsLutEntries : 1];
+  const DigitLut lut = stage_lut<LUT, kCountThreads>(desc, slut);
 
   for (uint32_t i = threadIdx.x; i < nb; i += kCountThreads) h[i] = 0;
   if (threadIdx.x == 0) sh_or = 0;
@@ -430,7 +459,7 @@ __global__ __launch_bounds__(kCountThreads) void count_kernel(
     const int e = k * kCountThreads + threadIdx.x;
     if (e < cnt) {
       const U u = xf(raw[k]);
-      atomicAdd(&h[pass_digit<LUT>(u, P.shift, mask, lut, lut_shift)], 1u);
+      atomicAdd(&h[pass_digit<LUT>(u, P.shift, mask, lut)], 1u);
       vor |= u ^ uref;
     }
   }
@@ -776,7 +805,7 @@ template <typename KT, typename U, bool LUT>
 __device__ __forceinline__ void scatter_process_tile(
     const SortDesc* __restrict__ desc, const SegPlan* __restrict__ plan, ScatterLds& L,
     const TileInfo& ti, int ncols, const uint64_t (&v0)[kScatterItems],
-    uint64_t (&v1)[kScatterItems], int64_t my_off, const int32_t* lut) {
+    uint64_t (&v1)[kScatterItems], int64_t my_off, const DigitLut& lut) {
   constexpr int NT = kScatterThreads;
   constexpr int IT = kScatterItems;
   constexpr int NW = NT / 64;
@@ -790,14 +819,13 @@ __device__ __forceinline__ void scatter_process_tile(
   xf.init(*desc);
   const int kbytes = desc->key_bits >> 3;
   const uint64_t kmask = kbytes == 8 ? ~0ull : ((1ull << (8 * kbytes)) - 1);
-  const int lut_shift = desc->lut_shift;
   STAMP_DECL
   STAMP();
 
   lds_barrier();  // the previous tile's readers of L are done
   for (uint32_t i = threadIdx.x; i < (uint32_t)(NW * kMaxBins); i += NT) (&L.wc[0][0])[i] = 0;
   auto digit = [&](int k) -> uint32_t {
-    return pass_digit<LUT>(xf((U)(v0[k] & kmask)), P.shift, mask, lut, lut_shift);
+    return pass_digit<LUT>(xf((U)(v0[k] & kmask)), P.shift, mask, lut);
   };
   auto valid = [&](int k) -> bool { return ebase + k * 64 < cnt; };
   STAMP();  // 1: loads returned
@@ -852,30 +880,34 @@ __device__ __forceinline__ void scatter_process_tile(
         dout[i] = 0;
         if (j < cnt) {
           const uint64_t x = L.sval[j];
-          const uint32_t d = pass_digit<LUT>(xf((U)(x & kmask)), P.shift, mask, lut, lut_shift);
+          const uint32_t d = pass_digit<LUT>(xf((U)(x & kmask)), P.shift, mask, lut);
           dout[i] = (uint16_t)d;
           SCATTER_STORE<decltype(W_)::value>(out + ((int64_t)j + SCATTER_DST(d)) * (int64_t)st, x);
         }
       }
     });
   }
+  // Columns 1..: column c is staged from v1, then column c+1's loads are
+  // issued into the same registers before column c's stores, so their
+  // latency hides behind the stores (no extra VGPRs).
   for (int c = 1; c < ncols; c++) {
     const uint32_t cw = desc->cols[c].width, cst = desc->cols[c].stride;
-    if (c > 1) {
-      const char* src = desc->cols[c].base[P.buf];
-with_width(cw, [&](auto W_) {
-#pragma unroll
-  for (int k = 0; k < IT; k++) {
-    const int e = ebase + k * 64;
-    v1[k] = e < cnt ? ldw<decltype(W_)::value>(src + (ti.base + e) * (int64_t)cst) : 0;
-  }
-});
-    }
     lds_barrier();  // every slot of the previous column has been read
 #pragma unroll
     for (int k = 0; k < IT; k++)
       if (valid(k)) L.sval[pos[k]] = v1[k];
     lds_barrier();
+    if (c + 1 < ncols) {
+      const char* src = desc->cols[c + 1].base[P.buf];
+      const uint32_t nst = desc->cols[c + 1].stride;
+      with_width(desc->cols[c + 1].width, [&](auto W_) {
+#pragma unroll
+        for (int k = 0; k < IT; k++) {
+          const int e = ebase + k * 64;
+          v1[k] = e < cnt ? ldw<decltype(W_)::value>(src + (ti.base + e) * (int64_t)nst) : 0;
+        }
+      });
+    }
     char* out = desc->cols[c].base[P.dst];
     with_width(cw, [&](auto W_) {
 #pragma unroll
@@ -897,7 +929,7 @@ __global__ __launch_bounds__(kScatterThreads, SRS_SCATTER_WAVES_PER_EU) void sca
     const SortDesc* __restrict__ desc, const SegPlan* __restrict__ plan,
     const int32_t* __restrict__ tile_seg, const uint64_t* __restrict__ offs) {
   __shared__ ScatterLds L;
-  __shared__ int32_t slut[LUT ? (1 << kLdsLutBits) : 1];
+  __shared__ uint16_t slut[LUT ? kLdsLutEntries : 1];
   const int64_t t = xcd_remap(blockIdx.x, gridDim.x);
   const int ncols = desc->ncols;
   uint64_t v0[kScatterItems], v1[kScatterItems];
@@ -905,7 +937,7 @@ __global__ __launch_bounds__(kScatterThreads, SRS_SCATTER_WAVES_PER_EU) void sca
   const TileInfo ti = scatter_load_tile<KT, U>(desc, plan, tile_seg, offs, t, ncols, v0, v1, my_off);
   if (ti.cnt == 0) return;
   // (the table is published by the barrier at the top of the tile)
-  const int32_t* lut = stage_lut<LUT, kScatterThreads>(desc, slut);
+  const DigitLut lut = stage_lut<LUT, kScatterThreads>(desc, slut);
   scatter_process_tile<KT, U, LUT>(desc, plan, L, ti, ncols, v0, v1, my_off, lut);
 }
 
@@ -919,8 +951,8 @@ __global__ __launch_bounds__(kScatterThreads, SRS_SCATTER_WAVES_PER_EU) void sca
     const SortDesc* __restrict__ desc, const SegPlan* __restrict__ plan,
     const int32_t* __restrict__ tile_seg, const uint64_t* __restrict__ offs, int64_t ntiles) {
   __shared__ ScatterLds L;
-  __shared__ int32_t slut[LUT ? (1 << kLdsLutBits) : 1];
-  const int32_t* lut = stage_lut<LUT, kScatterThreads>(desc, slut);
+  __shared__ uint16_t slut[LUT ? kLdsLutEntries : 1];
+  const DigitLut lut = stage_lut<LUT, kScatterThreads>(desc, slut);
   const int64_t G = gridDim.x;
   const int64_t r = xcd_remap(blockIdx.x, G);
   if (r >= ntiles) return;

@@ -91,7 +91,8 @@ def _kernel_resources():
 
 def test_hot_kernels_keep_their_occupancy():
     """The occupancy the tuning relies on: two 16-wave scatter
-    workgroups per CU need <= 64 VGPRs (8 waves/SIMD); count 8 waves/SIMD;
+    workgroups per CU need <= 64 VGPRs (8 waves/SIMD), with or without the
+    24 KB digit table; count 8 waves/SIMD (6 for digit-table passes);
     the small local class 6 waves/SIMD (3 workgroups of 8 waves); nothing
     on the hot path spills to scratch."""
     res = _kernel_resources()
@@ -105,5 +106,7 @@ def test_hot_kernels_keep_their_occupancy():
             assert r.get("ScratchSize", 0) == 0, (name, r)
             if key == "local_kernelI":
                 occ = 6 if "Li512ELi8ELi6E" in name else 4
+            if key == "count_kernel" and "Lb1E" in name:
+                occ = 6  # digit-table (LUT) passes stage a 26 KB table in LDS
             assert r["Occupancy"] >= occ, (name, r)
     assert seen == set(need)
