@@ -1358,9 +1358,14 @@ with_width(w, [&](auto W_) {
   lds_barrier();
   const unsigned long long var = sh_or;
 
+  // exact: the bucket digit covers every varying bit, so each bucket holds a
+  // single key value and the stable bucket pass alone is the sorted order
+  bool exact = false;
+  uint16_t* sidx = (uint16_t*)sbuf;  // exact case: original index by output slot
   if (var != 0) {
     const int lo = __ffsll((long long)var) - 1;
     const int hi = 63 - __clzll((long long)var);
+    exact = hi - lo + 1 <= kLocalTopBits;
     // the sort word packs (key bits 0..hi, original index): needs hi+1+IDXB <= 64
     if (hi + 1 + IDXB > 64) {
       if (threadIdx.x == 0) fallback[atomicAdd(fallback_count, 1ull)] = g;
@@ -1404,10 +1409,12 @@ with_width(w, [&](auto W_) {
       if (valid(k)) {
         const uint32_t d = digit(k);
         const uint32_t p = bin_start[d] + wc_perm[wave * NB + d] + rank[k];
-        sbuf[p] = (((uint64_t)ukey(k) & keep) << IDXB) | (uint64_t)(ebase + k * 64);
+        if (exact) sidx[p] = (uint16_t)(ebase + k * 64);
+        else sbuf[p] = (((uint64_t)ukey(k) & keep) << IDXB) | (uint64_t)(ebase + k * 64);
       }
     }
     lds_barrier();
+    if (!exact) {
     // ---- 3. buckets whose keys all equal are final (the pass was stable) --
 #pragma unroll
     for (int i = 0; i < IT; i++) {
@@ -1479,6 +1486,7 @@ with_width(w, [&](auto W_) {
       }
     }
     lds_barrier();
+    }  // !exact
   } else if (g.buf == BUF_OUT) {
     continue;  // all keys equal and already home
   } else {
@@ -1489,7 +1497,7 @@ with_width(w, [&](auto W_) {
   // output slot e takes input element perm[e]
   uint32_t id[IT];
 #pragma unroll
-  for (int k = 0; k < IT; k++) id[k] = perm[ebase + k * 64];
+  for (int k = 0; k < IT; k++) id[k] = exact ? sidx[ebase + k * 64] : perm[ebase + k * 64];
 
   // ---- 5. columns, software-pipelined as in local_kernel -------------------
   auto load_col = [&](int c, uint64_t (&dst)[IT]) {
