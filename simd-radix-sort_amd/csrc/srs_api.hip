@@ -497,7 +497,6 @@ int run_sort(Workspace* W, const Request& R, hipStream_t st) {
   SRS_TRY(ensure(W->ctr, sizeof(ListCounters)));
   SRS_TRY(ensure(W->totals, 4 * sizeof(uint64_t)));
   ListCounters* d_ctr = (ListCounters*)W->ctr.p;
-  uint64_t* d_totals = (uint64_t*)W->totals.p;
   int64_t n_big = 0, n_local = 0, n_local2 = 0, n_copy = 0;
   if (R.nsegs > 0) {
     // independent segments (multi-GPU receive groups): sorted as sub-ranges
@@ -583,14 +582,10 @@ int run_sort(Workspace* W, const Request& R, hipStream_t st) {
     }
     {
       TimedScope ts2("local_stable", 0, st);
-      // one workgroup per listed segment up to a cap (the list length is
-      // only known on device; surplus workgroups exit at once)
-      if (n_local2 > 0)
-        launch_local_stable(ks, d_desc, fb, nfb, 1, fb2, nfb2,
-                            (int)std::min<int64_t>(SRS_STABLE_GRID_MAX, n_local2), st);
-      if (n_local > 0)
-        launch_local_stable(ks, d_desc, fb1, nfb1, 0, fb2, nfb2,
-                            (int)std::min<int64_t>(SRS_STABLE_GRID_MAX, n_local), st);
+      // one workgroup per segment that could have been handed over (the
+      // list length is only known on device; surplus workgroups exit at once)
+      if (n_local2 > 0) launch_local_stable(ks, d_desc, fb, nfb, 1, fb2, nfb2, (int)n_local2, st);
+      if (n_local > 0) launch_local_stable(ks, d_desc, fb1, nfb1, 0, fb2, nfb2, (int)n_local, st);
     }
     {
       TimedScope ts3("local_lsd", 0, st);

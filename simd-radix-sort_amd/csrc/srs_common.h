@@ -94,17 +94,8 @@ struct ListCounters {
 #ifndef SRS_SCATTER_WAVES_PER_EU
 #define SRS_SCATTER_WAVES_PER_EU 8
 #endif
-#ifndef SRS_SCATTER_PIPE
-#define SRS_SCATTER_PIPE 0
-#endif
-#ifndef SRS_SCATTER_WG_PER_CU
-#define SRS_SCATTER_WG_PER_CU 2
-#endif
 #ifndef SRS_LOCAL_RANK_SPLIT
 #define SRS_LOCAL_RANK_SPLIT 2
-#endif
-#ifndef SRS_LOCAL_KEEP_KEYS
-#define SRS_LOCAL_KEEP_KEYS 0
 #endif
 constexpr int kScatterThreads = SRS_SCATTER_THREADS;
 constexpr int kScatterItems = SRS_SCATTER_ITEMS;
@@ -131,9 +122,6 @@ constexpr int kLdsLutEntries = 4096 + 16 * 512; // two-level table worst case (2
 #endif
 #ifndef SRS_LOCAL_ITEMS
 #define SRS_LOCAL_ITEMS 8
-#endif
-#ifndef SRS_STABLE_GRID_MAX
-#define SRS_STABLE_GRID_MAX (1 << 30)
 #endif
 constexpr int kLocalItems = SRS_LOCAL_ITEMS;
 constexpr int kLocalThreads = SRS_LOCAL_THREADS;

@@ -58,14 +58,6 @@ __device__ __forceinline__ void stw(char* p, uint64_t v) {
 }
 
 template <int W>
-__device__ __forceinline__ void stw_nt(char* p, uint64_t v) {
-  if constexpr (W == 1) __builtin_nontemporal_store((uint8_t)v, (uint8_t*)p);
-  else if constexpr (W == 2) __builtin_nontemporal_store((uint16_t)v, (uint16_t*)p);
-  else if constexpr (W == 4) __builtin_nontemporal_store((uint32_t)v, (uint32_t*)p);
-  else __builtin_nontemporal_store(v, (uint64_t*)p);
-}
-
-template <int W>
 struct WidthTag {
   static constexpr int value = W;
 };
@@ -417,7 +409,7 @@ __device__ __forceinline__ DigitLut stage_lut(const SortDesc* desc, uint16_t* sl
 }
 
 // ---------------------------------------------------------------------------
-// count: per-tile digit histogram (bin-major per segment) + varying bits
+// count: per-tile digit histogram (one tile-major row per tile) + varying bits
 // ---------------------------------------------------------------------------
 template <typename KT, typename U, bool LUT>
 __global__ __launch_bounds__(kCountThreads) void count_kernel(
@@ -736,16 +728,6 @@ __global__ __launch_bounds__(kMaxBins) void tile_offs_kernel(
 // store would wait for it). HBM then always has a tile's worth of loads in
 // flight per workgroup, and neighbouring tiles' runs into one bucket are
 // written by one workgroup (their partial lines meet in one L2).
-#if SRS_SCATTER_NT
-#define SCATTER_STORE stw_nt
-#else
-#define SCATTER_STORE stw
-#endif
-#if SRS_DEBUG_SEQ_WRITE  // timing experiment only: every tile written in place, unsorted order
-#define SCATTER_DST(d) (ti.base)
-#else
-#define SCATTER_DST(d) (L.gdst[d])
-#endif
 struct ScatterLds {
   uint64_t sval[kTile];
   uint16_t wc[kScatterThreads / 64][kMaxBins];
@@ -882,7 +864,7 @@ __device__ __forceinline__ void scatter_process_tile(
           const uint64_t x = L.sval[j];
           const uint32_t d = pass_digit<LUT>(xf((U)(x & kmask)), P.shift, mask, lut);
           dout[i] = (uint16_t)d;
-          SCATTER_STORE<decltype(W_)::value>(out + ((int64_t)j + SCATTER_DST(d)) * (int64_t)st, x);
+          stw<decltype(W_)::value>(out + ((int64_t)j + L.gdst[d]) * (int64_t)st, x);
         }
       }
     });
@@ -914,8 +896,8 @@ __device__ __forceinline__ void scatter_process_tile(
       for (int i = 0; i < IT; i++) {
         const int j = i * NT + (int)threadIdx.x;
         if (j < cnt)
-          SCATTER_STORE<decltype(W_)::value>(
-              out + ((int64_t)j + SCATTER_DST(dout[i])) * (int64_t)cst, L.sval[j]);
+          stw<decltype(W_)::value>(out + ((int64_t)j + L.gdst[dout[i]]) * (int64_t)cst,
+                                   L.sval[j]);
       }
     });
   }
@@ -939,39 +921,6 @@ __global__ __launch_bounds__(kScatterThreads, SRS_SCATTER_WAVES_PER_EU) void sca
   // (the table is published by the barrier at the top of the tile)
   const DigitLut lut = stage_lut<LUT, kScatterThreads>(desc, slut);
   scatter_process_tile<KT, U, LUT>(desc, plan, L, ti, ncols, v0, v1, my_off, lut);
-}
-
-// Persistent, software-pipelined: in round i the grid covers tiles
-// [i*G, (i+1)*G), XCD-aware inside the round (so that, as in the one-shot
-// kernel, tiles running at the same time are neighbours and their partial
-// bucket lines meet in one L2); a workgroup issues its next tile's loads
-// before ranking and storing the current one.
-template <typename KT, typename U, bool LUT>
-__global__ __launch_bounds__(kScatterThreads, SRS_SCATTER_WAVES_PER_EU) void scatter_pipe_kernel(
-    const SortDesc* __restrict__ desc, const SegPlan* __restrict__ plan,
-    const int32_t* __restrict__ tile_seg, const uint64_t* __restrict__ offs, int64_t ntiles) {
-  __shared__ ScatterLds L;
-  __shared__ uint16_t slut[LUT ? kLdsLutEntries : 1];
-  const DigitLut lut = stage_lut<LUT, kScatterThreads>(desc, slut);
-  const int64_t G = gridDim.x;
-  const int64_t r = xcd_remap(blockIdx.x, G);
-  if (r >= ntiles) return;
-  const int ncols = desc->ncols;
-  uint64_t a0[kScatterItems], a1[kScatterItems], b0[kScatterItems], b1[kScatterItems];
-  int64_t aoff, boff;
-  TileInfo ta = scatter_load_tile<KT, U>(desc, plan, tile_seg, offs, r, ncols, a0, a1, aoff);
-  for (int64_t t = r; t < ntiles; t += 2 * G) {
-    TileInfo tb;
-    tb.cnt = 0;
-    if (t + G < ntiles)
-      tb = scatter_load_tile<KT, U>(desc, plan, tile_seg, offs, t + G, ncols, b0, b1, boff);
-    if (ta.cnt > 0) scatter_process_tile<KT, U, LUT>(desc, plan, L, ta, ncols, a0, a1, aoff, lut);
-    if (t + G >= ntiles) break;
-    ta.cnt = 0;
-    if (t + 2 * G < ntiles)
-      ta = scatter_load_tile<KT, U>(desc, plan, tile_seg, offs, t + 2 * G, ncols, a0, a1, aoff);
-    if (tb.cnt > 0) scatter_process_tile<KT, U, LUT>(desc, plan, L, tb, ncols, b0, b1, boff, lut);
-  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1512,18 +1461,14 @@ with_width(w, [&](auto W_) {
     });
   };
   uint64_t vn[IT];
-  if (SRS_LOCAL_KEEP_KEYS) {
-    if (ncols > 1) load_col(1, vn);
-  } else {
-    load_col(0, vn);
-  }
+  load_col(0, vn);  // (the keys are reloaded: keeping them costs occupancy)
   for (int c = 0; c < ncols; c++) {
     char* out = desc->cols[c].base[BUF_OUT];
     const uint32_t st = desc->cols[c].stride;
     uint64_t v[IT];
 #pragma unroll
-    for (int k = 0; k < IT; k++) v[k] = (SRS_LOCAL_KEEP_KEYS && c == 0) ? v0[k] : vn[k];
-    if ((!SRS_LOCAL_KEEP_KEYS || c >= 1) && c + 1 < ncols) load_col(c + 1, vn);
+    for (int k = 0; k < IT; k++) v[k] = vn[k];
+    if (c + 1 < ncols) load_col(c + 1, vn);
     lds_barrier();  // previous users of sbuf are done
 #pragma unroll
     for (int k = 0; k < IT; k++)
@@ -1775,19 +1720,6 @@ void launch_offsets(SegPlan* plan, int64_t nbig, const int32_t* group_seg, int64
 void launch_scatter(int key_size, const SortDesc* d, const SegPlan* plan,
                     const int32_t* tile_seg, const uint64_t* offs, int64_t ntiles, bool lut,
                     hipStream_t st) {
-#if SRS_SCATTER_PIPE
-  int dev = 0, cus = 256;
-  if (hipGetDevice(&dev) == hipSuccess)
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  const int64_t grid = std::min<int64_t>(ntiles, (int64_t)cus * SRS_SCATTER_WG_PER_CU);
-#define CALL(KT, U)                                                                        \
-  if (lut)                                                                                 \
-    scatter_pipe_kernel<KT, U, true><<<(unsigned)grid, kScatterThreads, 0, st>>>(          \
-        d, plan, tile_seg, offs, ntiles);                                                  \
-  else                                                                                     \
-    scatter_pipe_kernel<KT, U, false><<<(unsigned)grid, kScatterThreads, 0, st>>>(         \
-        d, plan, tile_seg, offs, ntiles)
-#else
 #define CALL(KT, U)                                                                         \
   if (lut)                                                                                  \
     scatter_kernel<KT, U, true><<<(unsigned)ntiles, kScatterThreads, 0, st>>>(d, plan, tile_seg, \
@@ -1795,7 +1727,6 @@ void launch_scatter(int key_size, const SortDesc* d, const SegPlan* plan,
   else                                                                                      \
     scatter_kernel<KT, U, false><<<(unsigned)ntiles, kScatterThreads, 0, st>>>(d, plan,       \
                                                                              tile_seg, offs)
-#endif
   SRS_KEY_DISPATCH(key_size, CALL)
 #undef CALL
 }
