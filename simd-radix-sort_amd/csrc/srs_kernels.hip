@@ -941,7 +941,10 @@ __global__ __launch_bounds__(kScatterThreads, SRS_SCATTER_WAVES_PER_EU) void sca
 //   4. every column is staged in LDS in input order and written in output
 //      order: coalesced both ways, and safe in place.
 constexpr int kLocalBits = 9;      // digit of the LSD fallback passes
-constexpr int kLocalTopBits = 10;  // bucket digit of the fast path
+#ifndef SRS_LOCAL_TOP_BITS
+#define SRS_LOCAL_TOP_BITS 10
+#endif
+constexpr int kLocalTopBits = SRS_LOCAL_TOP_BITS;  // bucket digit of the local passes
 constexpr int kRankSortMax = 64;   // largest bucket the rank step takes
 
 // Stable ballot-ranked digit pass (fallback path): writes (u, id) in digit
@@ -1014,8 +1017,8 @@ __global__ __launch_bounds__(NT, WPE) void local_kernel(const SortDesc* __restri
   constexpr int IDXB = CAP <= 4096 ? 12 : 13;  // bits of an index inside the segment
   static_assert((1 << IDXB) >= CAP, "index bits");
   constexpr int NB = 1 << kLocalTopBits;
-  constexpr int BPT = NB / NT;
-  static_assert(BPT >= 1 && BPT * NT == NB, "bins per thread");
+  constexpr int BPT = NB >= NT ? NB / NT : 1;  // bins per thread (threads >= NB idle)
+  static_assert(BPT * NT >= NB, "bins per thread");
   // sbuf: packed sort words during the sort, column staging afterwards
   __shared__ uint64_t sbuf[CAP];
   __shared__ uint16_t perm[CAP];          // output slot -> original index
@@ -1099,7 +1102,8 @@ with_width(w, [&](auto W_) {
       uint32_t tb[BPT], tsum = 0;
 #pragma unroll
       for (int q = 0; q < BPT; q++) {
-        tb[q] = hist[threadIdx.x * BPT + q];
+        const uint32_t b = threadIdx.x * BPT + q;
+        tb[q] = b < (uint32_t)NB ? hist[b] : 0;
         tsum += tb[q];
       }
       uint32_t tot;
@@ -1107,8 +1111,11 @@ with_width(w, [&](auto W_) {
       int mymax = 0;
 #pragma unroll
       for (int q = 0; q < BPT; q++) {
-        bin_start[threadIdx.x * BPT + q] = ex;
-        hist[threadIdx.x * BPT + q] = ex;  // becomes the insertion cursor
+        const uint32_t b = threadIdx.x * BPT + q;
+        if (b < (uint32_t)NB) {
+          bin_start[b] = ex;
+          hist[b] = ex;  // becomes the insertion cursor
+        }
         ex += tb[q];
         mymax = (int)tb[q] > mymax ? (int)tb[q] : mymax;
       }
@@ -1246,8 +1253,8 @@ __global__ __launch_bounds__(NT) void local_stable_kernel(
   constexpr int IDXB = CAP <= 4096 ? 12 : 13;  // bits of an index inside the segment
   static_assert((1 << IDXB) >= CAP, "index bits");
   constexpr int NB = 1 << kLocalTopBits;
-  constexpr int BPT = NB / NT;
-  static_assert(BPT >= 1 && BPT * NT == NB, "bins per thread");
+  constexpr int BPT = NB >= NT ? NB / NT : 1;  // bins per thread (threads >= NB idle)
+  static_assert(BPT * NT >= NB, "bins per thread");
   constexpr int WCP = NW * NB > CAP ? NW * NB : CAP;
   // sbuf: packed sort words during the sort, column staging afterwards
   __shared__ uint64_t sbuf[CAP];
@@ -1335,11 +1342,13 @@ with_width(w, [&](auto W_) {
       for (int q = 0; q < BPT; q++) {
         const uint32_t b = threadIdx.x * BPT + q;
         tb[q] = 0;
+        if (b < (uint32_t)NB) {
 #pragma unroll
-        for (int w = 0; w < NW; w++) {
-          const uint32_t c = wc_perm[w * NB + b];
-          wc_perm[w * NB + b] = (uint16_t)tb[q];
-          tb[q] += c;
+          for (int w = 0; w < NW; w++) {
+            const uint32_t c = wc_perm[w * NB + b];
+            wc_perm[w * NB + b] = (uint16_t)tb[q];
+            tb[q] += c;
+          }
         }
         tsum += tb[q];
       }
@@ -1347,7 +1356,8 @@ with_width(w, [&](auto W_) {
       uint32_t ex = block_excl_scan_lds<NT>(tsum, scan_sh, &tot);
 #pragma unroll
       for (int q = 0; q < BPT; q++) {
-        bin_start[threadIdx.x * BPT + q] = ex;
+        const uint32_t b = threadIdx.x * BPT + q;
+        if (b < (uint32_t)NB) bin_start[b] = ex;
         ex += tb[q];
       }
       if (threadIdx.x == 0) bin_start[NB] = tot;
@@ -1380,6 +1390,7 @@ with_width(w, [&](auto W_) {
 #pragma unroll
       for (int q = 0; q < BPT; q++) {
         const uint32_t b = threadIdx.x * BPT + q;
+        if (b >= (uint32_t)NB) continue;
         const int len = (int)(bin_start[b + 1] - bin_start[b]);
         if (bflag[b] && len > mymax) mymax = len;
       }
