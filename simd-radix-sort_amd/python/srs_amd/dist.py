@@ -97,7 +97,11 @@ class ShardSorter:
 
     def __init__(self, ops, n_local: int, payload_dtypes, key_dtype, device, bits: int = 12,
                  groups: int = 512, rounds: int = 4, slack: float = 1.25, group=None,
-                 chunk_bytes: int = 256 << 20):
+                 chunk_bytes: int = 256 << 20, stage_host: bool = False):
+        # stage_host: the messages travel through host memory (test mode:
+        # several gloo ranks sharing one GPU run the real kernels; RCCL
+        # cannot put two ranks on one device)
+        self.stage_host = stage_host
         self.ops = ops
         self.key_bits = 8 * torch.empty(0, dtype=key_dtype).element_size()
         self.bits = min(bits, self.key_bits)
@@ -186,6 +190,9 @@ class ShardSorter:
         rk = self.recv_keys[:total]
         rps = [b[:total] for b in self.recv_pays]
         cols = [(self.part_keys, rk)] + list(zip(self.part_pays, rps))
+        mcols = cols                                      # what the messages move
+        if self.stage_host:
+            mcols = [(sb[:n].cpu(), torch.empty(total, dtype=rb.dtype)) for sb, rb in cols]
         # 6: rounds of peer-to-peer moves; round r+1 is in flight before the
         # (host-synchronising) sort of round r's groups is queued
         def issue(r):
@@ -200,21 +207,34 @@ class ShardSorter:
                         if cnt == 0:
                             continue
                         a = roff[(g, src)]
-                        for sbuf, rbuf in cols:
+                        for (sbuf, rbuf), (_, mrbuf) in zip(cols, mcols):
                             if src == me:
                                 rbuf[a:a + cnt].copy_(sbuf[soff[g]:soff[g] + cnt])
                             else:
-                                self._msgs(p2p, dist.irecv, rbuf, a, cnt, src)
+                                self._msgs(p2p, dist.irecv, mrbuf, a, cnt, src)
                 elif counts[g]:
-                    for sbuf, _ in cols:
-                        self._msgs(p2p, dist.isend, sbuf, soff[g], counts[g], dst)
+                    for msbuf, _ in mcols:
+                        self._msgs(p2p, dist.isend, msbuf, soff[g], counts[g], dst)
             return dist.batch_isend_irecv(p2p) if p2p else []
+
+        def land(r):
+            """host-staged mode: the round's received pieces to the device"""
+            for g in owned[me]:
+                if rnd[g] != r:
+                    continue
+                for src in range(w):
+                    cnt, a = mat[src][g], roff[(g, src)]
+                    if src != me and cnt:
+                        for (_, rbuf), (_, mrbuf) in zip(cols, mcols):
+                            rbuf[a:a + cnt].copy_(mrbuf[a:a + cnt])
 
         pending = issue(0)
         for r in range(R):
             for req in pending:
                 req.wait()
             pending = issue(r + 1) if r + 1 < R else []
+            if self.stage_host:
+                land(r)
             mine = [g for g in owned[me] if rnd[g] == r]
             if mine:
                 bounds = [gbound[mine[0]][0]] + [gbound[g][1] for g in mine]
