@@ -731,7 +731,7 @@ __global__ __launch_bounds__(kMaxBins) void tile_offs_kernel(
 struct ScatterLds {
   uint64_t sval[kTile];
   uint16_t wc[kScatterThreads / 64][kMaxBins];
-  uint32_t bin_start[kMaxBins];
+  uint16_t bin_start[kMaxBins];  // tile offsets <= kTile fit 16 bits
   int64_t gdst[kMaxBins];
   uint32_t scan_sh[kScatterThreads / 64 + 1];
 };
