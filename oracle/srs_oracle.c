@@ -247,7 +247,7 @@ static int64_t sort_bit_seq(ctx_t* c, int bit_no, int64_t left, int64_t right,
   int64_t l = left, r = right;
   while (l <= r) {
     while (l <= r && (dir_up != is_bit_set(c, elem(c, 0, l), bit_no))) l++;
-    while (l <= r && (!dir_up != is_bit_set(c, elem(c, 0, r), bit_no))) r--;
+    while (l <= r && ((!dir_up) != is_bit_set(c, elem(c, 0, r), bit_no))) r--;
     if (l < r) {
       for (int s = 0; s < c->nstreams; s++) {
         copy_elem(c->tmp[s], elem(c, s, l), c->size[s]);
