@@ -17,6 +17,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <map>
 #include <mutex>
 #include <string>
@@ -31,6 +32,16 @@ namespace {
 
 thread_local std::string g_err = "no error";
 unsigned long long* g_stamp_acc = nullptr;  // srs_debug_set_stamp_buffer
+
+// SRS_TRACE_LEVELS=1: one stderr line per global level and per local stage
+// (segment counts; diagnostics only, costs one extra read-back per sort)
+bool trace_levels() {
+  static const bool on = [] {
+    const char* e = getenv("SRS_TRACE_LEVELS");
+    return e && *e && *e != '0';
+  }();
+  return on;
+}
 
 int fail(int code, const std::string& msg) {
   g_err = msg;
@@ -420,6 +431,11 @@ int run_level(Workspace* W, int ks, const SortDesc* d_desc, LevelState& S, int f
   S.n_local2 = (int64_t)W->h_ctr->n_local2;
   S.n_copy = (int64_t)W->h_ctr->n_copy;
   S.cur = nxt;
+  if (trace_levels())
+    fprintf(stderr, "[srs] level: %lld segs, %.0f keys, %lld tiles%s -> big %lld, local %lld, "
+            "local2 %lld, copy %lld\n", (long long)nbig, level_elems, (long long)ntiles,
+            lut ? " (lut)" : "", (long long)S.nbig, (long long)S.n_local,
+            (long long)S.n_local2, (long long)S.n_copy);
   return SRS_OK;
 }
 
@@ -592,13 +608,17 @@ int run_sort(Workspace* W, const Request& R, hipStream_t st) {
       const int fgrid = (int)std::min<int64_t>(512, n_local + n_local2);
       launch_local_lsd(ks, d_desc, fb2, nfb2, fgrid, st);
     }
-    if (timing_enabled()) {
+    if (timing_enabled() || trace_levels()) {
       // diagnostics: how many segments took each fallback
       ListCounters c;
       HIP_TRY(hipMemcpyAsync(&c, d_ctr, sizeof(c), hipMemcpyDeviceToHost, st));
       HIP_TRY(hipStreamSynchronize(st));
       note_elems("local_stable", (double)(c.n_fallback + c.n_fallback1));
       note_elems("local_lsd", (double)c.n_fallback2);
+      if (trace_levels())
+        fprintf(stderr, "[srs] local: %lld + %lld segs (%llu keys); stable fallback %llu + %llu, "
+                "lsd fallback %llu\n", (long long)n_local, (long long)n_local2,
+                c.local_elems, c.n_fallback1, c.n_fallback, c.n_fallback2);
     }
   }
   if (n_copy > 0) {

@@ -28,12 +28,28 @@ namespace srs {
 // ---------------------------------------------------------------------------
 // small device helpers
 // ---------------------------------------------------------------------------
+// Every column pointer is read from the SortDesc in memory, so the compiler
+// cannot infer its address space and would emit FLAT loads/stores. FLAT ops
+// count on lgkmcnt as well as vmcnt: every LDS wait (and the LDS-only
+// barrier) would then also wait for the wave's outstanding global stores and
+// loads. All data accesses therefore go through address_space(1) pointers
+// (global_load / global_store, SGPR base + VGPR offset).
+#define SRS_GLOBAL __attribute__((address_space(1)))
+template <typename T>
+__device__ __forceinline__ T gld(const void* p) {
+  return *(const SRS_GLOBAL T*)(p);
+}
+template <typename T>
+__device__ __forceinline__ void gst(void* p, T v) {
+  *(SRS_GLOBAL T*)(p) = v;
+}
+
 __device__ __forceinline__ uint64_t load_w(const char* p, uint32_t w) {
   switch (w) {
-    case 1: return *(const uint8_t*)p;
-    case 2: return *(const uint16_t*)p;
-    case 4: return *(const uint32_t*)p;
-    default: return *(const uint64_t*)p;
+    case 1: return gld<uint8_t>(p);
+    case 2: return gld<uint16_t>(p);
+    case 4: return gld<uint32_t>(p);
+    default: return gld<uint64_t>(p);
   }
 }
 
@@ -43,18 +59,18 @@ __device__ __forceinline__ uint64_t load_w(const char* p, uint32_t w) {
 // and local kernels ran 25-30 % slower).
 template <int W>
 __device__ __forceinline__ uint64_t ldw(const char* p) {
-  if constexpr (W == 1) return *(const uint8_t*)p;
-  else if constexpr (W == 2) return *(const uint16_t*)p;
-  else if constexpr (W == 4) return *(const uint32_t*)p;
-  else return *(const uint64_t*)p;
+  if constexpr (W == 1) return gld<uint8_t>(p);
+  else if constexpr (W == 2) return gld<uint16_t>(p);
+  else if constexpr (W == 4) return gld<uint32_t>(p);
+  else return gld<uint64_t>(p);
 }
 
 template <int W>
 __device__ __forceinline__ void stw(char* p, uint64_t v) {
-  if constexpr (W == 1) *(uint8_t*)p = (uint8_t)v;
-  else if constexpr (W == 2) *(uint16_t*)p = (uint16_t)v;
-  else if constexpr (W == 4) *(uint32_t*)p = (uint32_t)v;
-  else *(uint64_t*)p = v;
+  if constexpr (W == 1) gst<uint8_t>(p, (uint8_t)v);
+  else if constexpr (W == 2) gst<uint16_t>(p, (uint16_t)v);
+  else if constexpr (W == 4) gst<uint32_t>(p, (uint32_t)v);
+  else gst<uint64_t>(p, v);
 }
 
 template <int W>
@@ -74,10 +90,10 @@ __device__ __forceinline__ void with_width(uint32_t w, F&& f) {
 
 __device__ __forceinline__ void store_w(char* p, uint32_t w, uint64_t v) {
   switch (w) {
-    case 1: *(uint8_t*)p = (uint8_t)v; break;
-    case 2: *(uint16_t*)p = (uint16_t)v; break;
-    case 4: *(uint32_t*)p = (uint32_t)v; break;
-    default: *(uint64_t*)p = v; break;
+    case 1: gst<uint8_t>(p, (uint8_t)v); break;
+    case 2: gst<uint16_t>(p, (uint16_t)v); break;
+    case 4: gst<uint32_t>(p, (uint32_t)v); break;
+    default: gst<uint64_t>(p, v); break;
   }
 }
 
@@ -125,7 +141,7 @@ __device__ __forceinline__ uint32_t pass_digit(U u, int shift, uint32_t mask, co
       const uint32_t t = L.s[x >> 4];
       return (t & 0x8000u) ? L.s[4096 + ((t & 0x7fffu) << 4) + (uint32_t)(x & 15)] : t;
     }
-    return L.s ? (uint32_t)L.s[x] : (uint32_t)L.g[x];
+    return L.s ? (uint32_t)L.s[x] : (uint32_t)gld<int32_t>(L.g + x);
   }
   return (uint32_t)(u >> shift) & mask;
 }
@@ -396,11 +412,11 @@ __device__ __forceinline__ DigitLut stage_lut(const SortDesc* desc, uint16_t* sl
   if (L.mode == 1) {
     const int n = desc->lut_entries;  // 4096 + 16 per split bin (<= kLdsLutEntries)
     const uint16_t* src = (const uint16_t*)desc->digit_lut;
-    for (int i = threadIdx.x; i < n; i += NT) slut[i] = src[i];
+    for (int i = threadIdx.x; i < n; i += NT) slut[i] = gld<uint16_t>(src + i);
     L.s = slut;
   } else if (desc->lut_bits <= kLdsLutBits) {
     const int n = 1 << desc->lut_bits;
-    for (int i = threadIdx.x; i < n; i += NT) slut[i] = (uint16_t)desc->digit_lut[i];
+    for (int i = threadIdx.x; i < n; i += NT) slut[i] = (uint16_t)gld<int32_t>(desc->digit_lut + i);
     L.s = slut;
   } else {
     L.g = desc->digit_lut;
@@ -438,12 +454,12 @@ __global__ __launch_bounds__(kCountThreads) void count_kernel(
   const int64_t base = P.start + tl * kTile;
   const int64_t rem = P.len - tl * kTile;
   const int cnt = rem < kTile ? (int)rem : kTile;
-  const U uref = xf((U) * (const KT*)(kp + P.start * (int64_t)ks));
+  const U uref = xf((U)gld<KT>(kp + P.start * (int64_t)ks));
   U raw[kCountItems];
 #pragma unroll
   for (int k = 0; k < kCountItems; k++) {
     const int e = k * kCountThreads + threadIdx.x;
-    raw[k] = e < cnt ? (U) * (const KT*)(kp + (base + e) * (int64_t)ks) : (U)0;
+    raw[k] = e < cnt ? (U)gld<KT>(kp + (base + e) * (int64_t)ks) : (U)0;
   }
   U vor = 0;
 #pragma unroll
@@ -1029,12 +1045,6 @@ __global__ __launch_bounds__(NT, WPE) void local_kernel(const SortDesc* __restri
   __shared__ int maxlen;
 
   const Seg g = segs[blockIdx.x];
-  if (g.rbits <= kLocalTopBits) {
-    // the stable kernel's single ballot pass resolves every remaining bit
-    // (and duplicate-heavy data would overflow the rank step here anyway)
-    if (threadIdx.x == 0) fallback[atomicAdd(fallback_count, 1ull)] = g;
-    return;
-  }
   const uint32_t wave = threadIdx.x >> 6;
   const uint32_t lane = lane_id();
   const int ebase = (int)wave * IT * 64 + (int)lane;  // element of slot k: ebase + 64 k
@@ -1084,8 +1094,9 @@ with_width(w, [&](auto W_) {
   if (var != 0) {
     const int lo = __ffsll((long long)var) - 1;
     const int hi = 63 - __clzll((long long)var);
+    const bool exact = hi - lo + 1 <= kLocalTopBits;
     // the sort word packs (key bits 0..hi, original index): needs hi+1+IDXB <= 64
-    if (hi + 1 + IDXB > 64) {
+    if (!exact && hi + 1 + IDXB > 64) {
       if (threadIdx.x == 0) fallback[atomicAdd(fallback_count, 1ull)] = g;
       return;
     }
@@ -1093,6 +1104,59 @@ with_width(w, [&](auto W_) {
     const int sh = hi - nbits + 1;
     const uint32_t mask = (1u << nbits) - 1;
     const uint64_t keep = (hi == 63) ? ~0ull : ((1ull << (hi + 1)) - 1);
+    if (exact) {
+      // ---- exact: the digit covers every varying bit, so a bucket holds one
+      // key value and a STABLE bucket pass (ballot ranks, input order inside
+      // a bucket) is the final order. Duplicate-heavy data (C2's floats) lands
+      // here; no bucket-size limit. Per-wave counters live in sbuf.
+      uint16_t* wc = (uint16_t*)sbuf;
+      static_assert(NW * NB * sizeof(uint16_t) <= CAP * sizeof(uint64_t), "wc fits sbuf");
+      const uint32_t nb = 1u << nbits;
+      for (uint32_t i = threadIdx.x; i < (uint32_t)(NW * NB / 4); i += NT)
+        ((uint64_t*)wc)[i] = 0;
+      auto digit = [&](int k) -> uint32_t { return (uint32_t)(ukey(k) >> lo) & mask; };
+      lds_barrier();
+      uint32_t rank[IT];
+      wlms_rank_fn<IT, kLocalTopBits>(digit, valid, nbits, &wc[wave * NB], rank);
+      lds_barrier();
+      {
+        uint32_t tb[BPT], tsum = 0;
+#pragma unroll
+        for (int q = 0; q < BPT; q++) {
+          const uint32_t b = threadIdx.x * BPT + q;
+          tb[q] = 0;
+          if (b < nb) {
+#pragma unroll
+            for (int w = 0; w < NW; w++) {
+              const uint32_t c = wc[w * NB + b];
+              wc[w * NB + b] = (uint16_t)tb[q];
+              tb[q] += c;
+            }
+          }
+          tsum += tb[q];
+        }
+        uint32_t tot;
+        uint32_t ex = block_excl_scan_lds<NT>(tsum, scan_sh, &tot);
+#pragma unroll
+        for (int q = 0; q < BPT; q++) {
+          const uint32_t b = threadIdx.x * BPT + q;
+          if (b < nb) bin_start[b] = ex;
+          ex += tb[q];
+        }
+      }
+      lds_barrier();
+#pragma unroll
+      for (int k = 0; k < IT; k++) {
+        if (valid(k)) {
+          const uint32_t d = digit(k);
+          perm[bin_start[d] + wc[wave * NB + d] + rank[k]] = (uint16_t)(ebase + k * 64);
+        }
+      }
+      lds_barrier();
+      STAMP();  // 2: stable bucket pass
+      STAMP();
+      STAMP();
+    } else {
     // ---- 2. bucket pass on the top varying bits (LDS atomics) -------------
 #pragma unroll
     for (int k = 0; k < IT; k++)
@@ -1184,6 +1248,7 @@ with_width(w, [&](auto W_) {
     }
     lds_barrier();
     STAMP();  // 4: ranked
+    }  // atomic bucket pass + rank
   } else if (g.buf == BUF_OUT) {
     return;  // all keys equal and already home
   } else {
