@@ -451,6 +451,7 @@ int run_sort(Workspace* W, const Request& R, hipStream_t st) {
   key_masks(R.kind, R.up, d);
   const bool is_float = R.kind == SRS_KEY_F32 || R.kind == SRS_KEY_F64;
   d.canon_zero = (is_float && n <= R.thresh) ? 1 : 0;
+  const int ksl = ks | (d.canon_zero ? SRS_KS_CANON : 0);  // kernel dispatch key
 
   size_t tmp_bytes = 0;
   std::vector<size_t> tmp_off;
@@ -567,12 +568,12 @@ int run_sort(Workspace* W, const Request& R, hipStream_t st) {
   int level = 0;
   if (balanced && S.nbig > 0) {
     ++level;
-    SRS_TRY(run_level(W, ks, d_desc, S, kMaxDigitBits, true, st,
+    SRS_TRY(run_level(W, ksl, d_desc, S, kMaxDigitBits, true, st,
                       (const int32_t*)W->lut_rbits.p));
   }
   while (S.nbig > 0) {
     if (++level > 80) return fail(SRS_ERR_INTERNAL, "level limit exceeded");
-    SRS_TRY(run_level(W, ks, d_desc, S, 0, false, st));
+    SRS_TRY(run_level(W, ksl, d_desc, S, 0, false, st));
   }
   n_local = S.n_local;
   n_local2 = S.n_local2;
@@ -593,20 +594,20 @@ int run_sort(Workspace* W, const Request& R, hipStream_t st) {
     unsigned long long* nfb2 = &d_ctr->n_fallback2;
     {
       TimedScope ts1("local_fast", 0, st);
-      if (n_local2 > 0) launch_local(ks, d_desc, (Seg*)W->local2.p, n_local2, 1, fb, nfb, st);
-      if (n_local > 0) launch_local(ks, d_desc, (Seg*)W->local.p, n_local, 0, fb1, nfb1, st);
+      if (n_local2 > 0) launch_local(ksl, d_desc, (Seg*)W->local2.p, n_local2, 1, fb, nfb, st);
+      if (n_local > 0) launch_local(ksl, d_desc, (Seg*)W->local.p, n_local, 0, fb1, nfb1, st);
     }
     {
       TimedScope ts2("local_stable", 0, st);
       // one workgroup per segment that could have been handed over (the
       // list length is only known on device; surplus workgroups exit at once)
-      if (n_local2 > 0) launch_local_stable(ks, d_desc, fb, nfb, 1, fb2, nfb2, (int)n_local2, st);
-      if (n_local > 0) launch_local_stable(ks, d_desc, fb1, nfb1, 0, fb2, nfb2, (int)n_local, st);
+      if (n_local2 > 0) launch_local_stable(ksl, d_desc, fb, nfb, 1, fb2, nfb2, (int)n_local2, st);
+      if (n_local > 0) launch_local_stable(ksl, d_desc, fb1, nfb1, 0, fb2, nfb2, (int)n_local, st);
     }
     {
       TimedScope ts3("local_lsd", 0, st);
       const int fgrid = (int)std::min<int64_t>(512, n_local + n_local2);
-      launch_local_lsd(ks, d_desc, fb2, nfb2, fgrid, st);
+      launch_local_lsd(ksl, d_desc, fb2, nfb2, fgrid, st);
     }
     if (timing_enabled() || trace_levels()) {
       // diagnostics: how many segments took each fallback

@@ -107,6 +107,9 @@ constexpr int kCountThreads = SRS_COUNT_THREADS;         // count kernel: one ti
 constexpr int kCountItems = kTile / kCountThreads;
 static_assert(kCountItems * kCountThreads == kTile, "count block shape");
 constexpr int kMaxDigitBits = 9;
+// launch_* key_size flag: the canon-zero float case (SortDesc::canon_zero),
+// selects the kernel instantiations that map -0.0 to +0.0
+#define SRS_KS_CANON 0x100
 constexpr int kMaxBins = 1 << kMaxDigitBits;   // histogram row stride (tile-major)
 static_assert(kScatterThreads >= kMaxBins, "the scatter tile scan gives one bin per thread");
 constexpr int kScanGroup = 256;                 // tiles per column-scan group

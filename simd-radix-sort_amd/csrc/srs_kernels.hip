@@ -99,20 +99,31 @@ __device__ __forceinline__ void store_w(char* p, uint32_t w, uint64_t v) {
 
 // Key transform (the reference's bitDirUp table, radixSort.hpp:1568-1581,
 // folded into one xor): unsigned order of u == the reference's key order.
-template <typename U>
+//   u = bits ^ (sign ? mneg : mpos) = bits ^ mpos ^ (s & (mpos ^ mneg)),
+// s = the key's sign bit smeared over the word (one v_ashr / v_bfe_i32), so a
+// key costs ~5 VALU (u64) instead of a 64-bit select. CZ: the n <= thresh
+// float case (SortDesc::canon_zero) maps -0.0 to +0.0 first; kernels are
+// instantiated with CZ only for that case (SRS_KS_CANON in the dispatch).
+template <typename U, bool CZ = false>
 struct Xform {
-  U mpos, mneg, signbit, negzero;
+  U mpos, cdiff, negzero;
+  int sbit;
   bool canon;
   __device__ __forceinline__ void init(const SortDesc& d) {
     mpos = (U)d.mpos;
-    mneg = (U)d.mneg;
-    signbit = (U)d.signbit;
+    cdiff = (U)(d.mpos ^ d.mneg);
     negzero = (U)d.negzero;
+    sbit = d.key_bits - 1;
     canon = d.canon_zero != 0;
   }
   __device__ __forceinline__ U operator()(U bits) const {
-    if (canon && bits == negzero) bits = 0;
-    return bits ^ ((bits & signbit) ? mneg : mpos);
+    if constexpr (CZ) {
+      if (canon && bits == negzero) bits = 0;
+    }
+    U sm;
+    if constexpr (sizeof(U) == 8) sm = (U)((int64_t)bits >> 63);  // U64 only holds 8-byte keys
+    else sm = (U)__builtin_amdgcn_sbfe((int)bits, sbit, 1);
+    return bits ^ mpos ^ (sm & cdiff);
   }
 };
 
@@ -251,31 +262,48 @@ __device__ __forceinline__ T block_excl_scan_lds(T v, T* sh, T* total) {
   return r;
 }
 
+// Peer mask of a lane's digit: the lanes of the wave whose digit equals it
+// (and that are valid), one ballot per digit bit. Per bit: x = 0 / ~0 from
+// the lane's bit (v_bfe_i32), m = ballot, peers &= ~(m ^ x) (v_bitop3 on
+// gfx950). FIXED: all MAXB bits unconditionally (digits must be < 2^MAXB;
+// zero high bits leave the mask unchanged), no per-bit predication;
+// otherwise a uniform runtime loop over nbits.
+template <int MAXB, bool FIXED>
+__device__ __forceinline__ uint64_t wlms_peers(uint32_t d, bool ok, int nbits) {
+  const uint64_t v = __ballot(ok);
+  uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+  auto step = [&](int b) {
+    const uint32_t x = (uint32_t)__builtin_amdgcn_sbfe((int)d, b, 1);
+    const uint64_t m = __ballot(x != 0);
+    lo &= ~((uint32_t)m ^ x);
+    hi &= ~((uint32_t)(m >> 32) ^ x);
+  };
+  if constexpr (FIXED) {
+#pragma unroll
+    for (int b = 0; b < MAXB; b++) step(b);
+  } else {
+    for (int b = 0; b < nbits; b++) step(b);
+  }
+  return ((uint64_t)hi << 32) | lo;
+}
+
 // Wave-level multisplit rank (stable): for each item slot k, lanes whose
-// digit matches form a peer group found with `nbits` ballots; the rank of a
-// key is the wave's running count of its digit (per-wave LDS counter row
-// `wc`) plus the number of lower-lane peers. Items are in striped order
-// (slot k of lane l = wave-local element k * 64 + l), so ranks follow input
-// order within a digit.
-template <int ITEMS, int MAXB = kMaxDigitBits, typename DigitFn, typename ValidFn>
+// digit matches form a peer group (wlms_peers); the rank of a key is the
+// wave's running count of its digit (per-wave LDS counter row `wc`) plus
+// the number of lower-lane peers. Items are in striped order (slot k of lane
+// l = wave-local element k * 64 + l), so ranks follow input order within a
+// digit.
+template <int ITEMS, int MAXB = kMaxDigitBits, bool FIXED = false, typename DigitFn,
+          typename ValidFn>
 __device__ __forceinline__ void wlms_rank_fn(DigitFn digit, ValidFn valid, int nbits,
                                              uint16_t* wc, uint32_t (&rank)[ITEMS]) {
-  const uint64_t lt = (lane_id() == 0) ? 0ull : (~0ull >> (64 - lane_id()));
 #pragma unroll
   for (int k = 0; k < ITEMS; k++) {
     const bool ok = valid(k);
-    uint64_t peers = __ballot(ok);
     const uint32_t d = digit(k);
-#pragma unroll
-    for (int b = 0; b < MAXB; b++) {
-      if (b < nbits) {
-        const bool bit = (d >> b) & 1u;
-        const uint64_t m = __ballot(bit);
-        peers &= bit ? m : ~m;
-      }
-    }
+    const uint64_t peers = wlms_peers<MAXB, FIXED>(d, ok, nbits);
     if (ok) {
-      const uint32_t below = (uint32_t)__popcll(peers & lt);
+      const uint32_t below = popc_below(peers);
       const uint32_t base = wc[d];
       rank[k] = base + below;
       if (below == 0) wc[d] = (uint16_t)(base + (uint32_t)__popcll(peers));
@@ -287,26 +315,8 @@ template <int ITEMS>
 __device__ __forceinline__ void wlms_rank(const uint32_t (&dig)[ITEMS],
                                           const bool (&valid)[ITEMS], int nbits,
                                           uint16_t* wc, uint32_t (&rank)[ITEMS]) {
-  const uint64_t lt = (lane_id() == 0) ? 0ull : (~0ull >> (64 - lane_id()));
-#pragma unroll
-  for (int k = 0; k < ITEMS; k++) {
-    uint64_t peers = __ballot(valid[k]);
-    const uint32_t d = dig[k];
-#pragma unroll
-    for (int b = 0; b < kMaxDigitBits; b++) {
-      if (b < nbits) {
-        const bool bit = (d >> b) & 1u;
-        const uint64_t m = __ballot(bit);
-        peers &= bit ? m : ~m;
-      }
-    }
-    if (valid[k]) {
-      const uint32_t below = (uint32_t)__popcll(peers & lt);
-      const uint32_t base = wc[d];
-      rank[k] = base + below;
-      if (below == 0) wc[d] = (uint16_t)(base + (uint32_t)__popcll(peers));
-    }
-  }
+  wlms_rank_fn<ITEMS, kMaxDigitBits, false>([&](int k) { return dig[k]; },
+                                            [&](int k) { return valid[k]; }, nbits, wc, rank);
 }
 
 // ---------------------------------------------------------------------------
@@ -427,7 +437,7 @@ __device__ __forceinline__ DigitLut stage_lut(const SortDesc* desc, uint16_t* sl
 // ---------------------------------------------------------------------------
 // count: per-tile digit histogram (one tile-major row per tile) + varying bits
 // ---------------------------------------------------------------------------
-template <typename KT, typename U, bool LUT>
+template <typename KT, typename U, bool LUT, bool CZ>
 __global__ __launch_bounds__(kCountThreads) void count_kernel(
     const SortDesc* __restrict__ desc, const SegPlan* __restrict__ plan,
     const int32_t* __restrict__ tile_seg, uint32_t* __restrict__ hist,
@@ -440,7 +450,7 @@ __global__ __launch_bounds__(kCountThreads) void count_kernel(
   const int64_t tl = t - P.tile_base;
   const uint32_t nb = 1u << P.bits;
   const uint32_t mask = nb - 1;
-  Xform<U> xf;
+  Xform<U, CZ> xf;
   xf.init(*desc);
   const char* kp = desc->key.base[P.buf];
   const uint32_t ks = desc->key.stride;
@@ -744,8 +754,12 @@ __global__ __launch_bounds__(kMaxBins) void tile_offs_kernel(
 // store would wait for it). HBM then always has a tile's worth of loads in
 // flight per workgroup, and neighbouring tiles' runs into one bucket are
 // written by one workgroup (their partial lines meet in one L2).
+template <bool LUT>
 struct ScatterLds {
   uint64_t sval[kTile];
+  // digit of each staged slot (LUT passes recompute it instead: their 24 KB
+  // table must leave room for two workgroups per CU)
+  uint16_t sdig[LUT ? 1 : kTile];
   uint16_t wc[kScatterThreads / 64][kMaxBins];
   uint16_t bin_start[kMaxBins];  // tile offsets <= kTile fit 16 bits
   int64_t gdst[kMaxBins];
@@ -799,9 +813,9 @@ with_width(w, [&](auto W_) {
   return ti;
 }
 
-template <typename KT, typename U, bool LUT>
+template <typename KT, typename U, bool LUT, bool CZ>
 __device__ __forceinline__ void scatter_process_tile(
-    const SortDesc* __restrict__ desc, const SegPlan* __restrict__ plan, ScatterLds& L,
+    const SortDesc* __restrict__ desc, const SegPlan* __restrict__ plan, ScatterLds<LUT>& L,
     const TileInfo& ti, int ncols, const uint64_t (&v0)[kScatterItems],
     uint64_t (&v1)[kScatterItems], int64_t my_off, const DigitLut& lut) {
   constexpr int NT = kScatterThreads;
@@ -813,7 +827,7 @@ __device__ __forceinline__ void scatter_process_tile(
   const uint32_t wave = threadIdx.x >> 6;
   const int ebase = (int)wave * IT * 64 + (int)lane_id();
   const int cnt = ti.cnt;
-  Xform<U> xf;
+  Xform<U, CZ> xf;
   xf.init(*desc);
   const int kbytes = desc->key_bits >> 3;
   const uint64_t kmask = kbytes == 8 ? ~0ull : ((1ull << (8 * kbytes)) - 1);
@@ -821,16 +835,21 @@ __device__ __forceinline__ void scatter_process_tile(
   STAMP();
 
   lds_barrier();  // the previous tile's readers of L are done
-  for (uint32_t i = threadIdx.x; i < (uint32_t)(NW * kMaxBins); i += NT) (&L.wc[0][0])[i] = 0;
-  auto digit = [&](int k) -> uint32_t {
-    return pass_digit<LUT>(xf((U)(v0[k] & kmask)), P.shift, mask, lut);
-  };
+  for (uint32_t i = threadIdx.x; i < (uint32_t)(NW * kMaxBins / 4); i += NT)
+    ((uint64_t*)&L.wc[0][0])[i] = 0;
   auto valid = [&](int k) -> bool { return ebase + k * 64 < cnt; };
+  // each key's digit, computed once (transform + digit cost ~15 VALU per key)
+  uint32_t dg[IT];
+#pragma unroll
+  for (int k = 0; k < IT; k++) dg[k] = pass_digit<LUT>(xf((U)(v0[k] & kmask)), P.shift, mask, lut);
   STAMP();  // 1: loads returned
   lds_barrier();  // wc zeroed
 
   uint32_t pos[IT];
-  wlms_rank_fn<IT>(digit, valid, P.bits, &L.wc[wave][0], pos);
+  // digits are < 2^kMaxDigitBits: every ballot unconditionally (no per-bit
+  // predication); bits above P.bits are zero in every lane
+  wlms_rank_fn<IT, kMaxDigitBits, true>([&](int k) { return dg[k]; }, valid, P.bits,
+                                        &L.wc[wave][0], pos);
   lds_barrier();
   STAMP();  // 2: ranked
 
@@ -858,15 +877,16 @@ __device__ __forceinline__ void scatter_process_tile(
 #pragma unroll
   for (int k = 0; k < IT; k++) {
     if (valid(k)) {
-      const uint32_t d = digit(k);
+      const uint32_t d = dg[k];
       pos[k] = L.bin_start[d] + L.wc[wave][d] + pos[k];
       L.sval[pos[k]] = v0[k];
+      if constexpr (!LUT) L.sdig[pos[k]] = (uint16_t)d;
     }
   }
   lds_barrier();
   STAMP();  // 4: column 0 staged
 
-  // column 0: output slot j's bucket comes from the key itself
+  // column 0: output slot j's bucket was staged with it
   uint16_t dout[IT];
   {
     char* out = desc->cols[0].base[P.dst];
@@ -878,7 +898,9 @@ __device__ __forceinline__ void scatter_process_tile(
         dout[i] = 0;
         if (j < cnt) {
           const uint64_t x = L.sval[j];
-          const uint32_t d = pass_digit<LUT>(xf((U)(x & kmask)), P.shift, mask, lut);
+          uint32_t d;
+          if constexpr (LUT) d = pass_digit<LUT>(xf((U)(x & kmask)), P.shift, mask, lut);
+          else d = L.sdig[j];
           dout[i] = (uint16_t)d;
           stw<decltype(W_)::value>(out + ((int64_t)j + L.gdst[d]) * (int64_t)st, x);
         }
@@ -922,11 +944,11 @@ __device__ __forceinline__ void scatter_process_tile(
 }
 
 // One tile per workgroup (XCD-aware order).
-template <typename KT, typename U, bool LUT>
+template <typename KT, typename U, bool LUT, bool CZ>
 __global__ __launch_bounds__(kScatterThreads, SRS_SCATTER_WAVES_PER_EU) void scatter_kernel(
     const SortDesc* __restrict__ desc, const SegPlan* __restrict__ plan,
     const int32_t* __restrict__ tile_seg, const uint64_t* __restrict__ offs) {
-  __shared__ ScatterLds L;
+  __shared__ ScatterLds<LUT> L;
   __shared__ uint16_t slut[LUT ? kLdsLutEntries : 1];
   const int64_t t = xcd_remap(blockIdx.x, gridDim.x);
   const int ncols = desc->ncols;
@@ -936,7 +958,7 @@ __global__ __launch_bounds__(kScatterThreads, SRS_SCATTER_WAVES_PER_EU) void sca
   if (ti.cnt == 0) return;
   // (the table is published by the barrier at the top of the tile)
   const DigitLut lut = stage_lut<LUT, kScatterThreads>(desc, slut);
-  scatter_process_tile<KT, U, LUT>(desc, plan, L, ti, ncols, v0, v1, my_off, lut);
+  scatter_process_tile<KT, U, LUT, CZ>(desc, plan, L, ti, ncols, v0, v1, my_off, lut);
 }
 
 // ---------------------------------------------------------------------------
@@ -1023,7 +1045,7 @@ __device__ __forceinline__ void local_digit_pass(
 // Fast path: bucket pass with LDS atomics (order inside a bucket arbitrary);
 // the rank step then restores the stable order from the packed
 // (key bits, original index) words.
-template <typename KT, typename U, int NT, int IT, int WPE>
+template <typename KT, typename U, int NT, int IT, int WPE, bool CZ>
 __global__ __launch_bounds__(NT, WPE) void local_kernel(const SortDesc* __restrict__ desc,
                                                    const Seg* __restrict__ segs,
                                                    Seg* __restrict__ fallback,
@@ -1048,7 +1070,7 @@ __global__ __launch_bounds__(NT, WPE) void local_kernel(const SortDesc* __restri
   const uint32_t wave = threadIdx.x >> 6;
   const uint32_t lane = lane_id();
   const int ebase = (int)wave * IT * 64 + (int)lane;  // element of slot k: ebase + 64 k
-  Xform<U> xf;
+  Xform<U, CZ> xf;
   xf.init(*desc);
   const int cnt = (int)g.len;
   const int64_t base = g.start;
@@ -1307,7 +1329,7 @@ with_width(w, [&](auto W_) {
 // larger than kRankSortMax): the bucket pass ranks with ballots (stable), so
 // buckets whose keys are all equal are final; only mixed buckets are ranked.
 // Grid-stride over a device-side list whose length is read on device.
-template <typename KT, typename U, int NT>
+template <typename KT, typename U, int NT, bool CZ>
 __global__ __launch_bounds__(NT) void local_stable_kernel(
     const SortDesc* __restrict__ desc, const Seg* __restrict__ segs,
     const unsigned long long* __restrict__ nsegs, Seg* __restrict__ fallback,
@@ -1334,7 +1356,7 @@ __global__ __launch_bounds__(NT) void local_stable_kernel(
   const uint32_t wave = threadIdx.x >> 6;
   const uint32_t lane = lane_id();
   const int ebase = (int)wave * IT * 64 + (int)lane;  // element of slot k: ebase + 64 k
-  Xform<U> xf;
+  Xform<U, CZ> xf;
   xf.init(*desc);
   const int ncols = desc->ncols;
   const int kbytes = desc->key_bits >> 3;
@@ -1565,7 +1587,7 @@ with_width(w, [&](auto W_) {
 // Fallback for segments whose top-digit buckets are too large for the rank
 // step (skewed keys): stable LSD passes (ballot ranks) over every varying
 // bit. Grid-stride over a device-side list whose length is read on device.
-template <typename KT, typename U>
+template <typename KT, typename U, bool CZ>
 __global__ __launch_bounds__(kLocalStableThreads) void local_lsd_kernel(
     const SortDesc* __restrict__ desc, const Seg* __restrict__ segs,
     const unsigned long long* __restrict__ nsegs) {
@@ -1583,7 +1605,7 @@ __global__ __launch_bounds__(kLocalStableThreads) void local_lsd_kernel(
   U* su = (U*)sbuf;
   const uint32_t wave = threadIdx.x >> 6;
   const int ebase = (int)wave * IT * 64 + (int)lane_id();
-  Xform<U> xf;
+  Xform<U, CZ> xf;
   xf.init(*desc);
   const int ncols = desc->ncols;
   const int kbytes = desc->key_bits >> 3;
@@ -1729,12 +1751,15 @@ __global__ void fill_kernel(int64_t n, int kind, uint64_t seed, uint64_t first,
 // ---------------------------------------------------------------------------
 // launch wrappers (host side, called from srs_api.hip)
 // ---------------------------------------------------------------------------
-#define SRS_KEY_DISPATCH(KSZ, CALL)                 \
-  switch (KSZ) {                                     \
-    case 1: CALL(uint8_t, uint32_t); break;          \
-    case 2: CALL(uint16_t, uint32_t); break;         \
-    case 4: CALL(uint32_t, uint32_t); break;         \
-    default: CALL(uint64_t, uint64_t); break;        \
+// KSZ: key size in bytes, | SRS_KS_CANON for the canon-zero float case
+#define SRS_KEY_DISPATCH(KSZ, CALL)                              \
+  switch (KSZ) {                                                  \
+    case 1: CALL(uint8_t, uint32_t, false); break;                \
+    case 2: CALL(uint16_t, uint32_t, false); break;               \
+    case 4: CALL(uint32_t, uint32_t, false); break;               \
+    case 4 | SRS_KS_CANON: CALL(uint32_t, uint32_t, true); break; \
+    case 8 | SRS_KS_CANON: CALL(uint64_t, uint64_t, true); break; \
+    default: CALL(uint64_t, uint64_t, false); break;              \
   }
 
 void launch_plan(const Seg* big, int64_t nbig, SegPlan* plan, int64_t* tcount,
@@ -1759,13 +1784,13 @@ void launch_seg_map(const int64_t* bases, int64_t nbig, int64_t n, int32_t* out,
 void launch_count(int key_size, const SortDesc* d, const SegPlan* plan,
                   const int32_t* tile_seg, int64_t ntiles, uint32_t* hist,
                   unsigned long long* var_or, bool lut, hipStream_t st) {
-#define CALL(KT, U)                                                                        \
-  if (lut)                                                                                 \
-    count_kernel<KT, U, true><<<(unsigned)ntiles, kCountThreads, 0, st>>>(d, plan, tile_seg, \
-                                                                          hist, var_or);   \
-  else                                                                                     \
-    count_kernel<KT, U, false><<<(unsigned)ntiles, kCountThreads, 0, st>>>(d, plan, tile_seg, \
-                                                                           hist, var_or)
+#define CALL(KT, U, CZ)                                                                 \
+  if (lut)                                                                              \
+    count_kernel<KT, U, true, CZ><<<(unsigned)ntiles, kCountThreads, 0, st>>>(            \
+        d, plan, tile_seg, hist, var_or);                                               \
+  else                                                                                  \
+    count_kernel<KT, U, false, CZ><<<(unsigned)ntiles, kCountThreads, 0, st>>>(           \
+        d, plan, tile_seg, hist, var_or)
   SRS_KEY_DISPATCH(key_size, CALL)
 #undef CALL
 }
@@ -1796,25 +1821,25 @@ void launch_offsets(SegPlan* plan, int64_t nbig, const int32_t* group_seg, int64
 void launch_scatter(int key_size, const SortDesc* d, const SegPlan* plan,
                     const int32_t* tile_seg, const uint64_t* offs, int64_t ntiles, bool lut,
                     hipStream_t st) {
-#define CALL(KT, U)                                                                         \
-  if (lut)                                                                                  \
-    scatter_kernel<KT, U, true><<<(unsigned)ntiles, kScatterThreads, 0, st>>>(d, plan, tile_seg, \
-                                                                            offs);          \
-  else                                                                                      \
-    scatter_kernel<KT, U, false><<<(unsigned)ntiles, kScatterThreads, 0, st>>>(d, plan,       \
-                                                                             tile_seg, offs)
+#define CALL(KT, U, CZ)                                                                 \
+  if (lut)                                                                              \
+    scatter_kernel<KT, U, true, CZ><<<(unsigned)ntiles, kScatterThreads, 0, st>>>(        \
+        d, plan, tile_seg, offs);                                                       \
+  else                                                                                  \
+    scatter_kernel<KT, U, false, CZ><<<(unsigned)ntiles, kScatterThreads, 0, st>>>(       \
+        d, plan, tile_seg, offs)
   SRS_KEY_DISPATCH(key_size, CALL)
 #undef CALL
 }
 
 void launch_local(int key_size, const SortDesc* d, const Seg* segs, int64_t nsegs, int big_class,
                   Seg* fallback, unsigned long long* fallback_count, hipStream_t st) {
-#define CALL(KT, U)                                                                  \
-  if (big_class)                                                                     \
-    local_kernel<KT, U, kLocalThreads, kLocalItems, kLocalWavesPerEU>                \
-        <<<(unsigned)nsegs, kLocalThreads, 0, st>>>(d, segs, fallback, fallback_count); \
-  else                                                                               \
-    local_kernel<KT, U, kLocalThreadsSmall, kLocalItemsSmall, kLocalWavesPerEUSmall> \
+#define CALL(KT, U, CZ)                                                                  \
+  if (big_class)                                                                         \
+    local_kernel<KT, U, kLocalThreads, kLocalItems, kLocalWavesPerEU, CZ>                \
+        <<<(unsigned)nsegs, kLocalThreads, 0, st>>>(d, segs, fallback, fallback_count);  \
+  else                                                                                   \
+    local_kernel<KT, U, kLocalThreadsSmall, kLocalItemsSmall, kLocalWavesPerEUSmall, CZ> \
         <<<(unsigned)nsegs, kLocalThreadsSmall, 0, st>>>(d, segs, fallback, fallback_count)
   SRS_KEY_DISPATCH(key_size, CALL)
 #undef CALL
@@ -1823,13 +1848,13 @@ void launch_local(int key_size, const SortDesc* d, const Seg* segs, int64_t nseg
 void launch_local_stable(int key_size, const SortDesc* d, const Seg* segs,
                          const unsigned long long* nsegs, int big_class, Seg* fallback,
                          unsigned long long* fallback_count, int grid, hipStream_t st) {
-#define CALL(KT, U)                                                                    \
+#define CALL(KT, U, CZ)                                                                \
   if (big_class)                                                                       \
-    local_stable_kernel<KT, U, kLocalStableThreads>                                    \
+    local_stable_kernel<KT, U, kLocalStableThreads, CZ>                                \
         <<<(unsigned)grid, kLocalStableThreads, 0, st>>>(d, segs, nsegs, fallback,      \
                                                          fallback_count);              \
   else                                                                                 \
-    local_stable_kernel<KT, U, kLocalStableThreadsSmall>                               \
+    local_stable_kernel<KT, U, kLocalStableThreadsSmall, CZ>                           \
         <<<(unsigned)grid, kLocalStableThreadsSmall, 0, st>>>(d, segs, nsegs, fallback, \
                                                              fallback_count)
   SRS_KEY_DISPATCH(key_size, CALL)
@@ -1838,8 +1863,8 @@ void launch_local_stable(int key_size, const SortDesc* d, const Seg* segs,
 
 void launch_local_lsd(int key_size, const SortDesc* d, const Seg* segs,
                       const unsigned long long* nsegs, int grid, hipStream_t st) {
-#define CALL(KT, U) \
-  local_lsd_kernel<KT, U><<<(unsigned)grid, kLocalStableThreads, 0, st>>>(d, segs, nsegs)
+#define CALL(KT, U, CZ) \
+  local_lsd_kernel<KT, U, CZ><<<(unsigned)grid, kLocalStableThreads, 0, st>>>(d, segs, nsegs)
   SRS_KEY_DISPATCH(key_size, CALL)
 #undef CALL
 }
@@ -1876,7 +1901,8 @@ __global__ __launch_bounds__(256) void key_hist_kernel(int64_t n, const KT* __re
 void launch_key_hist(int key_size, int64_t n, const void* keys, const SortDesc& d, int bits,
                      unsigned long long* hist, hipStream_t st) {
   const int grid = (int)std::min<int64_t>(2048, (n + 255) / 256);
-#define CALL(KT, U) key_hist_kernel<KT, U><<<grid, 256, 0, st>>>(n, (const KT*)keys, d, bits, hist)
+#define CALL(KT, U, CZ) \
+  key_hist_kernel<KT, U><<<grid, 256, 0, st>>>(n, (const KT*)keys, d, bits, hist)
   SRS_KEY_DISPATCH(key_size, CALL)
 #undef CALL
 }

@@ -460,3 +460,26 @@ def test_scale_float_keys_vs_torch_stable(dist):
     assert torch.equal(ko.view(torch.int32 if kind == srs_amd.KEY_F32 else torch.int64),
                        ref_k.view(torch.int32 if kind == srs_amd.KEY_F32 else torch.int64))
     assert torch.equal(po, ref_i)
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+@pytest.mark.parametrize("n", [3000, 70000])
+@pytest.mark.parametrize("up", [True, False])
+def test_float_zero_canon_large_threshold(dtype, n, up):
+    """n <= cmpSortThreshold with many -0.0/+0.0 keys: the reference's leaf
+    compares by value (-0.0 == +0.0, input order kept), radixSort.hpp:1743 +
+    :159-178. With a threshold >= n the GPU runs the canon-zero kernel
+    instantiations (SRS_KS_CANON) through the local (n=3000) and the global
+    levels (n=70000); a threshold of 16 must keep -0.0 before +0.0."""
+    rng = np.random.default_rng(n + (dtype == np.float64))
+    keys = rng.choice(np.array([-0.0, 0.0, 1.5, -2.25, 0.5, -0.0, 0.0], dtype=dtype), n)
+    mix = rng.random(n) < 0.3
+    keys[mix] = rng.standard_normal(int(mix.sum())).astype(dtype)
+    pay = np.arange(n, dtype=np.uint32)
+    kind = srs_amd.key_kind_of(keys.dtype)
+    for thresh in (n, 16):
+        k, p = keys.copy(), pay.copy()
+        srs_amd.sort_thresh(thresh, k, p, up=up)
+        ek, ep = stable_reference(kind, up, [keys, pay], thresh)
+        assert bytes_equal(k, ek), (thresh, "keys")
+        assert bytes_equal(p, ep), (thresh, "payload order")
