@@ -980,9 +980,10 @@ __global__ __launch_bounds__(kScatterThreads, SRS_SCATTER_WAVES_PER_EU) void sca
 //      order: coalesced both ways, and safe in place.
 constexpr int kLocalBits = 9;      // digit of the LSD fallback passes
 #ifndef SRS_LOCAL_TOP_BITS
-#define SRS_LOCAL_TOP_BITS 10
+#define SRS_LOCAL_TOP_BITS 11
 #endif
-constexpr int kLocalTopBits = SRS_LOCAL_TOP_BITS;  // bucket digit of the local passes
+constexpr int kLocalTopBits = SRS_LOCAL_TOP_BITS;  // bucket digit of the fast local kernel
+constexpr int kLocalStableTopBits = 10;            // bucket digit of the stable fallback
 constexpr int kRankSortMax = 64;   // largest bucket the rank step takes
 
 // Stable ballot-ranked digit pass (fallback path): writes (u, id) in digit
@@ -1055,13 +1056,14 @@ __global__ __launch_bounds__(NT, WPE) void local_kernel(const SortDesc* __restri
   constexpr int IDXB = CAP <= 4096 ? 12 : 13;  // bits of an index inside the segment
   static_assert((1 << IDXB) >= CAP, "index bits");
   constexpr int NB = 1 << kLocalTopBits;
-  constexpr int BPT = NB >= NT ? NB / NT : 1;  // bins per thread (threads >= NB idle)
-  static_assert(BPT * NT >= NB, "bins per thread");
+  constexpr int BPT = NB / NT;  // bins per thread (an even count: packed pairs)
+  static_assert(BPT * NT == NB && BPT % 2 == 0, "bins per thread");
+  static_assert(CAP < 65536, "16-bit bucket counters");
   // sbuf: packed sort words during the sort, column staging afterwards
   __shared__ uint64_t sbuf[CAP];
   __shared__ uint16_t perm[CAP];          // output slot -> original index
-  __shared__ uint32_t hist[NB];           // bucket sizes, then insertion cursors
-  __shared__ uint32_t bin_start[NB + 1];
+  __shared__ uint32_t hist2[NB / 2];      // 16-bit bucket sizes, then cursors (pairs)
+  __shared__ uint16_t bin_start[NB + 2];
   __shared__ uint32_t scan_sh[NW + 1];
   __shared__ unsigned long long sh_or;
   __shared__ int maxlen;
@@ -1084,7 +1086,7 @@ __global__ __launch_bounds__(NT, WPE) void local_kernel(const SortDesc* __restri
     sh_or = 0;
     maxlen = 0;
   }
-  for (uint32_t i = threadIdx.x; i < (uint32_t)NB; i += NT) hist[i] = 0;
+  for (uint32_t i = threadIdx.x; i < (uint32_t)(NB / 2); i += NT) hist2[i] = 0;
 
   // ---- 1. keys (column 0 holds the key in its low bytes) -------------------
   uint64_t v0[IT];
@@ -1130,16 +1132,15 @@ with_width(w, [&](auto W_) {
       // ---- exact: the digit covers every varying bit, so a bucket holds one
       // key value and a STABLE bucket pass (ballot ranks, input order inside
       // a bucket) is the final order. Duplicate-heavy data (C2's floats) lands
-      // here; no bucket-size limit. Per-wave counters live in sbuf.
+      // here; no bucket-size limit. Per-wave counters [NW][nb] live in sbuf.
       uint16_t* wc = (uint16_t*)sbuf;
       static_assert(NW * NB * sizeof(uint16_t) <= CAP * sizeof(uint64_t), "wc fits sbuf");
       const uint32_t nb = 1u << nbits;
-      for (uint32_t i = threadIdx.x; i < (uint32_t)(NW * NB / 4); i += NT)
-        ((uint64_t*)wc)[i] = 0;
+      for (uint32_t i = threadIdx.x; i < NW * nb / 2; i += NT) ((uint32_t*)wc)[i] = 0;
       auto digit = [&](int k) -> uint32_t { return (uint32_t)(ukey(k) >> lo) & mask; };
       lds_barrier();
       uint32_t rank[IT];
-      wlms_rank_fn<IT, kLocalTopBits>(digit, valid, nbits, &wc[wave * NB], rank);
+      wlms_rank_fn<IT, kLocalTopBits>(digit, valid, nbits, &wc[wave * nb], rank);
       lds_barrier();
       {
         uint32_t tb[BPT], tsum = 0;
@@ -1148,10 +1149,9 @@ with_width(w, [&](auto W_) {
           const uint32_t b = threadIdx.x * BPT + q;
           tb[q] = 0;
           if (b < nb) {
-#pragma unroll
             for (int w = 0; w < NW; w++) {
-              const uint32_t c = wc[w * NB + b];
-              wc[w * NB + b] = (uint16_t)tb[q];
+              const uint32_t c = wc[w * nb + b];
+              wc[w * nb + b] = (uint16_t)tb[q];
               tb[q] += c;
             }
           }
@@ -1162,7 +1162,7 @@ with_width(w, [&](auto W_) {
 #pragma unroll
         for (int q = 0; q < BPT; q++) {
           const uint32_t b = threadIdx.x * BPT + q;
-          if (b < nb) bin_start[b] = ex;
+          if (b < nb) bin_start[b] = (uint16_t)ex;
           ex += tb[q];
         }
       }
@@ -1171,7 +1171,7 @@ with_width(w, [&](auto W_) {
       for (int k = 0; k < IT; k++) {
         if (valid(k)) {
           const uint32_t d = digit(k);
-          perm[bin_start[d] + wc[wave * NB + d] + rank[k]] = (uint16_t)(ebase + k * 64);
+          perm[bin_start[d] + wc[wave * nb + d] + rank[k]] = (uint16_t)(ebase + k * 64);
         }
       }
       lds_barrier();
@@ -1179,33 +1179,39 @@ with_width(w, [&](auto W_) {
       STAMP();
       STAMP();
     } else {
-    // ---- 2. bucket pass on the top varying bits (LDS atomics) -------------
+    // ---- 2. bucket pass on the top varying bits (LDS atomics on 16-bit
+    // counters packed in pairs: 2^11 buckets in the LDS of 2^10 u32 ones) ----
 #pragma unroll
-    for (int k = 0; k < IT; k++)
-      if (valid(k)) atomicAdd(&hist[(uint32_t)(ukey(k) >> sh) & mask], 1u);
+    for (int k = 0; k < IT; k++) {
+      if (valid(k)) {
+        const uint32_t d = (uint32_t)(ukey(k) >> sh) & mask;
+        atomicAdd(&hist2[d >> 1], 1u << ((d & 1) << 4));
+      }
+    }
     lds_barrier();
     {
       uint32_t tb[BPT], tsum = 0;
 #pragma unroll
-      for (int q = 0; q < BPT; q++) {
-        const uint32_t b = threadIdx.x * BPT + q;
-        tb[q] = b < (uint32_t)NB ? hist[b] : 0;
-        tsum += tb[q];
+      for (int q = 0; q < BPT; q += 2) {
+        const uint32_t w2 = hist2[(threadIdx.x * BPT + q) >> 1];
+        tb[q] = w2 & 0xFFFFu;
+        tb[q + 1] = w2 >> 16;
+        tsum += tb[q] + tb[q + 1];
       }
       uint32_t tot;
       uint32_t ex = block_excl_scan_lds<NT>(tsum, scan_sh, &tot);
       int mymax = 0;
 #pragma unroll
-      for (int q = 0; q < BPT; q++) {
+      for (int q = 0; q < BPT; q += 2) {
         const uint32_t b = threadIdx.x * BPT + q;
-        if (b < (uint32_t)NB) {
-          bin_start[b] = ex;
-          hist[b] = ex;  // becomes the insertion cursor
-        }
-        ex += tb[q];
-        mymax = (int)tb[q] > mymax ? (int)tb[q] : mymax;
+        const uint32_t e0 = ex, e1 = ex + tb[q];
+        bin_start[b] = (uint16_t)e0;
+        bin_start[b + 1] = (uint16_t)e1;
+        hist2[b >> 1] = e0 | (e1 << 16);  // insertion cursors
+        ex = e1 + tb[q + 1];
+        mymax = max(mymax, (int)max(tb[q], tb[q + 1]));
       }
-      if (threadIdx.x == 0) bin_start[NB] = tot;
+      if (threadIdx.x == 0) bin_start[NB] = (uint16_t)tot;
       if (mymax > 0) atomicMax(&maxlen, mymax);
     }
     lds_barrier();
@@ -1220,7 +1226,9 @@ with_width(w, [&](auto W_) {
     for (int k = 0; k < IT; k++) {
       if (valid(k)) {
         const U uk = ukey(k);
-        const uint32_t p = atomicAdd(&hist[(uint32_t)(uk >> sh) & mask], 1u);
+        const uint32_t d = (uint32_t)(uk >> sh) & mask;
+        const uint32_t hs = (d & 1) << 4;
+        const uint32_t p = (atomicAdd(&hist2[d >> 1], 1u << hs) >> hs) & 0xFFFFu;
         sbuf[p] = (((uint64_t)uk & keep) << IDXB) | (uint64_t)(ebase + k * 64);
       }
     }
@@ -1257,10 +1265,19 @@ with_width(w, [&](auto W_) {
         const int t2 = __shfl_xor(wmax, o, 64);
         wmax = t2 > wmax ? t2 : wmax;
       }
-      for (int j = 0; j < wmax; j++) {
+      // Branch-free: every item reads a valid slot of its bucket (clamped
+      // to the last one) and masks the count, so the H reads of one step
+      // issue back to back under a single wait (a predicated read per item
+      // waited for each read in turn).
+      uint32_t last[H];
 #pragma unroll
-        for (int i = 0; i < H; i++)
-          if ((uint32_t)j < bl[i]) r[i] += sbuf[bs[i] + j] < x[i];
+      for (int i = 0; i < H; i++) last[i] = bs[i] + (bl[i] ? bl[i] - 1 : 0);
+      for (int j = 0; j < wmax; j++) {
+        uint64_t w[H];
+#pragma unroll
+        for (int i = 0; i < H; i++) w[i] = sbuf[min(bs[i] + (uint32_t)j, last[i])];
+#pragma unroll
+        for (int i = 0; i < H; i++) r[i] += ((uint32_t)j < bl[i]) & (w[i] < x[i]);
       }
 #pragma unroll
       for (int i = 0; i < H; i++) {
@@ -1339,7 +1356,7 @@ __global__ __launch_bounds__(NT) void local_stable_kernel(
   constexpr int CAP = NT * IT;
   constexpr int IDXB = CAP <= 4096 ? 12 : 13;  // bits of an index inside the segment
   static_assert((1 << IDXB) >= CAP, "index bits");
-  constexpr int NB = 1 << kLocalTopBits;
+  constexpr int NB = 1 << kLocalStableTopBits;
   constexpr int BPT = NB >= NT ? NB / NT : 1;  // bins per thread (threads >= NB idle)
   static_assert(BPT * NT >= NB, "bins per thread");
   constexpr int WCP = NW * NB > CAP ? NW * NB : CAP;
@@ -1408,20 +1425,20 @@ with_width(w, [&](auto W_) {
   if (var != 0) {
     const int lo = __ffsll((long long)var) - 1;
     const int hi = 63 - __clzll((long long)var);
-    exact = hi - lo + 1 <= kLocalTopBits;
+    exact = hi - lo + 1 <= kLocalStableTopBits;
     // the sort word packs (key bits 0..hi, original index): needs hi+1+IDXB <= 64
     if (hi + 1 + IDXB > 64) {
       if (threadIdx.x == 0) fallback[atomicAdd(fallback_count, 1ull)] = g;
       continue;
     }
-    const int nbits = (hi - lo + 1) < kLocalTopBits ? (hi - lo + 1) : kLocalTopBits;
+    const int nbits = (hi - lo + 1) < kLocalStableTopBits ? (hi - lo + 1) : kLocalStableTopBits;
     const int sh = hi - nbits + 1;
     const uint32_t mask = (1u << nbits) - 1;
     const uint64_t keep = (hi == 63) ? ~0ull : ((1ull << (hi + 1)) - 1);
     // ---- 2. stable bucket pass on the top varying bits (ballot ranks) -----
     auto digit = [&](int k) -> uint32_t { return (uint32_t)(ukey(k) >> sh) & mask; };
     uint32_t rank[IT];
-    wlms_rank_fn<IT, kLocalTopBits>(digit, valid, nbits, &wc_perm[wave * NB], rank);
+    wlms_rank_fn<IT, kLocalStableTopBits>(digit, valid, nbits, &wc_perm[wave * NB], rank);
     lds_barrier();
     {
       uint32_t tb[BPT], tsum = 0;
