@@ -19,6 +19,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <type_traits>
 
 #include "srs_common.h"
 #include "srs_kernels.h"
@@ -95,6 +96,48 @@ __device__ __forceinline__ void store_w(char* p, uint32_t w, uint64_t v) {
     case 4: gst<uint32_t>(p, (uint32_t)v); break;
     default: gst<uint64_t>(p, v); break;
   }
+}
+
+// Strip access: element ebase + 64 k (k < IT, element < cnt) of a column
+// whose element `first` is at `src`. Dense columns (stride == width) get
+// compile-time per-k offsets (one 64-bit address per strip, immediate
+// offsets after it); strided ones (AoS slices) a multiply per element.
+template <int IT, typename F>
+__device__ __forceinline__ void with_strip(uint32_t w, uint32_t st, F&& f) {
+  if (st == w)
+    with_width(w, [&](auto W_) { f(W_, std::integral_constant<bool, true>{}); });
+  else
+    with_width(w, [&](auto W_) { f(W_, std::integral_constant<bool, false>{}); });
+}
+
+template <int IT>
+__device__ __forceinline__ void load_strip(uint64_t (&dst)[IT], const char* src, uint32_t w,
+                                           uint32_t st, int64_t first, int ebase, int cnt) {
+  with_strip<IT>(w, st, [&](auto W_, auto D_) {
+    constexpr int W = decltype(W_)::value;
+    constexpr bool D = decltype(D_)::value;
+    const char* p0 = src + (first + ebase) * (int64_t)(D ? (uint32_t)W : st);
+#pragma unroll
+    for (int k = 0; k < IT; k++) {
+      const int64_t off = D ? (int64_t)k * 64 * W : (int64_t)k * 64 * st;
+      dst[k] = ebase + k * 64 < cnt ? ldw<W>(p0 + off) : 0;
+    }
+  });
+}
+
+template <int IT, typename V>
+__device__ __forceinline__ void store_strip(char* out, uint32_t w, uint32_t st, int64_t first,
+                                            int ebase, int cnt, V&& value) {
+  with_strip<IT>(w, st, [&](auto W_, auto D_) {
+    constexpr int W = decltype(W_)::value;
+    constexpr bool D = decltype(D_)::value;
+    char* p0 = out + (first + ebase) * (int64_t)(D ? (uint32_t)W : st);
+#pragma unroll
+    for (int k = 0; k < IT; k++) {
+      const int64_t off = D ? (int64_t)k * 64 * W : (int64_t)k * 64 * st;
+      if (ebase + k * 64 < cnt) stw<W>(p0 + off, value(k));
+    }
+  });
 }
 
 // Key transform (the reference's bitDirUp table, radixSort.hpp:1568-1581,
@@ -786,28 +829,11 @@ __device__ __forceinline__ TileInfo scatter_load_tile(
   const int64_t rem = P.len - tl * kTile;
   ti.cnt = P.skip ? 0 : (rem < kTile ? (int)rem : kTile);
   const int ebase = (int)(threadIdx.x >> 6) * IT * 64 + (int)lane_id();
-  {
-    const char* src = desc->cols[0].base[P.buf];
-    const uint32_t w = desc->cols[0].width, st = desc->cols[0].stride;
-with_width(w, [&](auto W_) {
-#pragma unroll
-  for (int k = 0; k < IT; k++) {
-    const int e = ebase + k * 64;
-    v0[k] = e < ti.cnt ? ldw<decltype(W_)::value>(src + (ti.base + e) * (int64_t)st) : 0;
-  }
-});
-  }
-  if (ncols > 1) {
-    const char* src = desc->cols[1].base[P.buf];
-    const uint32_t w = desc->cols[1].width, st = desc->cols[1].stride;
-with_width(w, [&](auto W_) {
-#pragma unroll
-  for (int k = 0; k < IT; k++) {
-    const int e = ebase + k * 64;
-    v1[k] = e < ti.cnt ? ldw<decltype(W_)::value>(src + (ti.base + e) * (int64_t)st) : 0;
-  }
-});
-  }
+  load_strip<IT>(v0, desc->cols[0].base[P.buf], desc->cols[0].width, desc->cols[0].stride,
+                 ti.base, ebase, ti.cnt);
+  if (ncols > 1)
+    load_strip<IT>(v1, desc->cols[1].base[P.buf], desc->cols[1].width, desc->cols[1].stride,
+                   ti.base, ebase, ti.cnt);
   my_off = 0;
   if (ti.cnt > 0 && threadIdx.x < (1u << P.bits)) my_off = (int64_t)offs[t * kMaxBins + threadIdx.x];
   return ti;
@@ -917,17 +943,9 @@ __device__ __forceinline__ void scatter_process_tile(
     for (int k = 0; k < IT; k++)
       if (valid(k)) L.sval[pos[k]] = v1[k];
     lds_barrier();
-    if (c + 1 < ncols) {
-      const char* src = desc->cols[c + 1].base[P.buf];
-      const uint32_t nst = desc->cols[c + 1].stride;
-      with_width(desc->cols[c + 1].width, [&](auto W_) {
-#pragma unroll
-        for (int k = 0; k < IT; k++) {
-          const int e = ebase + k * 64;
-          v1[k] = e < cnt ? ldw<decltype(W_)::value>(src + (ti.base + e) * (int64_t)nst) : 0;
-        }
-      });
-    }
+    if (c + 1 < ncols)
+      load_strip<IT>(v1, desc->cols[c + 1].base[P.buf], desc->cols[c + 1].width,
+                     desc->cols[c + 1].stride, ti.base, ebase, cnt);
     char* out = desc->cols[c].base[P.dst];
     with_width(cw, [&](auto W_) {
 #pragma unroll
@@ -1059,8 +1077,9 @@ __global__ __launch_bounds__(NT, WPE) void local_kernel(const SortDesc* __restri
   constexpr int BPT = NB / NT;  // bins per thread (an even count: packed pairs)
   static_assert(BPT * NT == NB && BPT % 2 == 0, "bins per thread");
   static_assert(CAP < 65536, "16-bit bucket counters");
-  // sbuf: packed sort words during the sort, column staging afterwards
-  __shared__ uint64_t sbuf[CAP];
+  // sbuf: packed sort words (+ rank sentinels) during the sort, column
+  // staging afterwards
+  __shared__ uint64_t sbuf[CAP + kRankSortMax];
   __shared__ uint16_t perm[CAP];          // output slot -> original index
   __shared__ uint32_t hist2[NB / 2];      // 16-bit bucket sizes, then cursors (pairs)
   __shared__ uint16_t bin_start[NB + 2];
@@ -1090,17 +1109,8 @@ __global__ __launch_bounds__(NT, WPE) void local_kernel(const SortDesc* __restri
 
   // ---- 1. keys (column 0 holds the key in its low bytes) -------------------
   uint64_t v0[IT];
-  {
-    const char* src = desc->cols[0].base[g.buf];
-    const uint32_t w = desc->cols[0].width, st = desc->cols[0].stride;
-with_width(w, [&](auto W_) {
-#pragma unroll
-  for (int k = 0; k < IT; k++) {
-    const int e = ebase + k * 64;
-    v0[k] = e < cnt ? ldw<decltype(W_)::value>(src + (base + e) * (int64_t)st) : 0;
-  }
-});
-  }
+  load_strip<IT>(v0, desc->cols[0].base[g.buf], desc->cols[0].width, desc->cols[0].stride, base,
+                 ebase, cnt);
   const U uref = xf((U)(load_w(desc->cols[0].base[g.buf] + base * (int64_t)desc->cols[0].stride,
                                desc->cols[0].width) & kmask));
   // keys are recomputed from v0 when needed (holding them costs occupancy)
@@ -1232,6 +1242,7 @@ with_width(w, [&](auto W_) {
         sbuf[p] = (((uint64_t)uk & keep) << IDXB) | (uint64_t)(ebase + k * 64);
       }
     }
+    if (threadIdx.x < (uint32_t)kRankSortMax) sbuf[cnt + threadIdx.x] = ~0ull;  // sentinels
     lds_barrier();
     STAMP();  // 3: bucket scatter
     // ---- 3. rank inside each bucket: #(words of the bucket below mine) ----
@@ -1265,19 +1276,16 @@ with_width(w, [&](auto W_) {
         const int t2 = __shfl_xor(wmax, o, 64);
         wmax = t2 > wmax ? t2 : wmax;
       }
-      // Branch-free: every item reads a valid slot of its bucket (clamped
-      // to the last one) and masks the count, so the H reads of one step
-      // issue back to back under a single wait (a predicated read per item
-      // waited for each read in turn).
-      uint32_t last[H];
-#pragma unroll
-      for (int i = 0; i < H; i++) last[i] = bs[i] + (bl[i] ? bl[i] - 1 : 0);
+      // Branch-free and unmasked: sbuf is in bucket order, so a word read
+      // past the end of my bucket belongs to a higher bucket (a larger key)
+      // or is a ~0 sentinel (slots [cnt, cnt + kRankSortMax)); neither is
+      // below x. The H reads of a step issue back to back under one wait.
       for (int j = 0; j < wmax; j++) {
         uint64_t w[H];
 #pragma unroll
-        for (int i = 0; i < H; i++) w[i] = sbuf[min(bs[i] + (uint32_t)j, last[i])];
+        for (int i = 0; i < H; i++) w[i] = sbuf[bs[i] + (uint32_t)j];
 #pragma unroll
-        for (int i = 0; i < H; i++) r[i] += ((uint32_t)j < bl[i]) & (w[i] < x[i]);
+        for (int i = 0; i < H; i++) r[i] += w[i] < x[i];
       }
 #pragma unroll
       for (int i = 0; i < H; i++) {
@@ -1306,21 +1314,12 @@ with_width(w, [&](auto W_) {
   // safe: a column's loads complete before the barrier that precedes its own
   // stores, and different columns never share bytes.
   auto load_col = [&](int c, uint64_t (&dst)[IT]) {
-    const char* src = desc->cols[c].base[g.buf];
-    const uint32_t st = desc->cols[c].stride;
-    with_width(desc->cols[c].width, [&](auto W_) {
-#pragma unroll
-      for (int k = 0; k < IT; k++) {
-        const int e = ebase + k * 64;
-        dst[k] = e < cnt ? ldw<decltype(W_)::value>(src + (base + e) * (int64_t)st) : 0;
-      }
-    });
+    load_strip<IT>(dst, desc->cols[c].base[g.buf], desc->cols[c].width, desc->cols[c].stride,
+                   base, ebase, cnt);
   };
   uint64_t vn[IT];
   if (ncols > 1) load_col(1, vn);
   for (int c = 0; c < ncols; c++) {
-    char* out = desc->cols[c].base[BUF_OUT];
-    const uint32_t st = desc->cols[c].stride;
     uint64_t v[IT];
 #pragma unroll
     for (int k = 0; k < IT; k++) v[k] = c == 0 ? v0[k] : vn[k];
@@ -1330,13 +1329,8 @@ with_width(w, [&](auto W_) {
     for (int k = 0; k < IT; k++)
       if (valid(k)) sbuf[ebase + k * 64] = v[k];
     lds_barrier();
-    with_width(desc->cols[c].width, [&](auto W_) {
-#pragma unroll
-      for (int k = 0; k < IT; k++) {
-        const int e = ebase + k * 64;
-        if (valid(k)) stw<decltype(W_)::value>(out + (base + e) * (int64_t)st, sbuf[id[k]]);
-      }
-    });
+    store_strip<IT>(desc->cols[c].base[BUF_OUT], desc->cols[c].width, desc->cols[c].stride, base,
+                    ebase, cnt, [&](int k) { return sbuf[id[k]]; });
     STAMP();  // 5, 6: column moved
   }
   STAMP_FLUSH(1);
