@@ -9,14 +9,14 @@ Protocol, per rank r holding n_r records (key + payload columns)
   4. stable partition of the local records into the G groups
                                                           (srs_partition_device)
      This IS the first MSB level of the sort: nothing is partitioned twice.
-  5. all-gather of the G group sizes of every rank; each rank lays out its
-     receive buffer group by group (sources in rank order inside a group),
-     so what arrives is already grouped by key range
+  5. all-gather of the G group sizes of every rank -> receive layout
   6. the groups move peer to peer (batched isend/irecv = RCCL grouped
-     send/recv over xGMI) in `rounds`, every message <= 256 MB (RCCL
-     corrupted a single 8 GB all_to_all message: measured at world 1, 1e9
-     int64; 1e8 was exact). While round i+1 is in flight, the groups of
-     round i are sorted on a second stream    (srs_sort_segments_device)
+     send/recv over xGMI) in `rounds`: round i moves a contiguous run of
+     each receiver's groups, one message per (round, peer, column), each
+     <= 256 MB (RCCL corrupted a single 8 GB all_to_all message: measured at
+     world 1, 1e9 int64; 1e8 was exact). A round lands source-major in its
+     own key range of the receive buffer; while round i+1 is in flight,
+     round i's range is sorted on a second stream (srs_sort_segments_device)
 Rank r then holds the r-th slice of the globally sorted array: every key on
 rank r orders before every key on rank r+1.
 
@@ -129,24 +129,20 @@ class ShardSorter:
                           for p in self.recv_pays]
 
     def plan(self, hist):
-        """bins -> groups (device int32, for the partition) and groups -> ranks
-        (host list), both non-decreasing."""
+        """bins -> groups (device int32, for the partition), groups -> ranks
+        (host list, non-decreasing) and each group's (first, last) bin."""
         G, w = self.groups, self.world
         group_of_bin = balanced_split(hist, G)
         gtot = torch.zeros(G, dtype=torch.int64, device=hist.device)
         gtot.index_add_(0, group_of_bin.to(torch.int64), hist.to(torch.int64))
         rank_of_group = balanced_split(gtot, w).tolist()
-        # top key bits shared inside each group: the common prefix of its
-        # first and last bin
         gb = group_of_bin.tolist()
         first, last = [None] * G, [None] * G
         for b, g in enumerate(gb):
             if first[g] is None:
                 first[g] = b
             last[g] = b
-        prefix = [0 if first[g] is None else self.bits - (first[g] ^ last[g]).bit_length()
-                  for g in range(G)]
-        return group_of_bin, rank_of_group, prefix
+        return group_of_bin, rank_of_group, first, last
 
     def sort(self, keys, pays):
         """Returns (keys, payloads) views: this rank's slice of the sorted union."""
@@ -159,7 +155,7 @@ class ShardSorter:
         # 1-3: global histogram -> key-range groups -> ranks
         hist = self.ops.histogram(keys, self.bits)
         dist.all_reduce(hist, group=self.group)
-        group_of_bin, rank_of_group, prefix = self.plan(hist)
+        group_of_bin, rank_of_group, first, last = self.plan(hist)
         # 4: stable partition into the groups (the first radix level)
         counts = self.ops.partition(keys, pays, self.bits, group_of_bin, G,
                                     (self.part_keys, *self.part_pays))
@@ -169,22 +165,31 @@ class ShardSorter:
         dist.all_gather(mat, send, group=self.group)
         mat = [m.tolist() for m in mat]                   # mat[src][g]
         owned = [[g for g in range(G) if rank_of_group[g] == r] for r in range(w)]
-        rnd = [0] * G                                     # exchange round of each group
-        for r in range(w):
-            for i, g in enumerate(owned[r]):
-                rnd[g] = i * R // max(1, len(owned[r]))
+        # exchange round r of rank d moves d's groups owned[d][rg[d][r]]: a
+        # contiguous run of groups, hence one contiguous piece of every
+        # sender's partitioned buffer
+        rg = [[range(i * len(owned[d]) // R, (i + 1) * len(owned[d]) // R) for i in range(R)]
+              for d in range(w)]
         soff = [0] * (G + 1)
         for g in range(G):
             soff[g + 1] = soff[g] + counts[g]
-        roff = {}                                         # (g, src) -> receive offset
-        gbound = {}                                       # g -> (start, end) in recv
-        pos = 0
-        for g in owned[me]:
+
+        def piece(src_counts, d, r):
+            """(first group, #records) of the round-r piece for rank d"""
+            gs = [owned[d][i] for i in rg[d][r]]
+            return (gs[0] if gs else 0), sum(src_counts[g] for g in gs)
+
+        # receive layout: round-major, then source-major (sources in rank
+        # order): one message per (round, peer, column). Equal keys share a
+        # group, so inside a round they arrive in (source rank, input index)
+        # order, and the round's key range lies above the previous round's.
+        roff, rbound, pos = {}, [], 0
+        for r in range(R):
             start = pos
             for src in range(w):
-                roff[(g, src)] = pos
-                pos += mat[src][g]
-            gbound[g] = (start, pos)
+                roff[(r, src)] = pos
+                pos += piece(mat[src], me, r)[1]
+            rbound.append((start, pos))
         total = pos
         self._ensure_capacity(total)
         rk = self.recv_keys[:total]
@@ -193,40 +198,38 @@ class ShardSorter:
         mcols = cols                                      # what the messages move
         if self.stage_host:
             mcols = [(sb[:n].cpu(), torch.empty(total, dtype=rb.dtype)) for sb, rb in cols]
+
         # 6: rounds of peer-to-peer moves; round r+1 is in flight before the
-        # (host-synchronising) sort of round r's groups is queued
+        # (host-synchronising) sort of round r is queued
         def issue(r):
             p2p = []
-            for g in range(G):
-                if rnd[g] != r:
-                    continue
-                dst = rank_of_group[g]
-                if dst == me:
+            for d in range(w):
+                g0, cnt = piece(counts, d, r)
+                if d == me:
                     for src in range(w):
-                        cnt = mat[src][g]
-                        if cnt == 0:
+                        rcnt = piece(mat[src], me, r)[1]
+                        if rcnt == 0:
                             continue
-                        a = roff[(g, src)]
+                        a = roff[(r, src)]
                         for (sbuf, rbuf), (_, mrbuf) in zip(cols, mcols):
                             if src == me:
-                                rbuf[a:a + cnt].copy_(sbuf[soff[g]:soff[g] + cnt])
+                                rbuf[a:a + rcnt].copy_(sbuf[soff[g0]:soff[g0] + rcnt])
                             else:
-                                self._msgs(p2p, dist.irecv, mrbuf, a, cnt, src)
-                elif counts[g]:
+                                self._msgs(p2p, dist.irecv, mrbuf, a, rcnt, src)
+                elif cnt:
                     for msbuf, _ in mcols:
-                        self._msgs(p2p, dist.isend, msbuf, soff[g], counts[g], dst)
+                        self._msgs(p2p, dist.isend, msbuf, soff[g0], cnt, d)
             return dist.batch_isend_irecv(p2p) if p2p else []
 
         def land(r):
             """host-staged mode: the round's received pieces to the device"""
-            for g in owned[me]:
-                if rnd[g] != r:
+            for src in range(w):
+                if src == me:
                     continue
-                for src in range(w):
-                    cnt, a = mat[src][g], roff[(g, src)]
-                    if src != me and cnt:
-                        for (_, rbuf), (_, mrbuf) in zip(cols, mcols):
-                            rbuf[a:a + cnt].copy_(mrbuf[a:a + cnt])
+                a, rcnt = roff[(r, src)], piece(mat[src], me, r)[1]
+                if rcnt:
+                    for (_, rbuf), (_, mrbuf) in zip(cols, mcols):
+                        rbuf[a:a + rcnt].copy_(mrbuf[a:a + rcnt])
 
         pending = issue(0)
         for r in range(R):
@@ -235,11 +238,28 @@ class ShardSorter:
             pending = issue(r + 1) if r + 1 < R else []
             if self.stage_host:
                 land(r)
-            mine = [g for g in owned[me] if rnd[g] == r]
-            if mine:
-                bounds = [gbound[mine[0]][0]] + [gbound[g][1] for g in mine]
-                known = min(min(prefix[g] for g in mine), self.key_bits - 1)
-                self.ops.sort_segments(rk, rps, bounds, known)
+            a, b = rbound[r]
+            gs = [owned[me][i] for i in rg[me][r]]
+            if b > a:
+                # top key bits shared by every segment's key range
+                def shared(grps):
+                    bins = [(first[g], last[g]) for g in grps if first[g] is not None]
+                    if not bins:
+                        return 0
+                    lo, hi = bins[0][0], bins[-1][1]
+                    return min(self.bits - (lo ^ hi).bit_length(), self.key_bits - 1)
+                if w == 1:
+                    # one source: the round's groups lie contiguous, each its
+                    # own segment (the partition was their first level)
+                    bounds = [a]
+                    for g in gs:
+                        bounds.append(bounds[-1] + counts[g])
+                    self.ops.sort_segments(rk, rps, bounds, min(shared([g]) for g in gs))
+                else:
+                    # several sources interleave the groups: the round's key
+                    # range is one segment (at w >= 2 its size needs no more
+                    # levels than a group's would)
+                    self.ops.sort_segments(rk, rps, [a, b], shared(gs))
         self.ops.finish(self.device)
         self.last_counts = (counts, [sum(mat[s][g] for g in owned[me]) for s in range(w)])
         return rk, rps
