@@ -803,7 +803,7 @@ struct ScatterLds {
   // digit of each staged slot (LUT passes recompute it instead: their 24 KB
   // table must leave room for two workgroups per CU)
   uint16_t sdig[LUT ? 1 : kTile];
-  uint16_t wc[kScatterThreads / 64][kMaxBins];
+  alignas(8) uint16_t wc[kScatterThreads / 64][kMaxBins];  // zeroed as u64
   uint16_t bin_start[kMaxBins];  // tile offsets <= kTile fit 16 bits
   int64_t gdst[kMaxBins];
   uint32_t scan_sh[kScatterThreads / 64 + 1];
