@@ -305,6 +305,22 @@ __device__ __forceinline__ T block_excl_scan_lds(T v, T* sh, T* total) {
   return r;
 }
 
+// Exclusive block scan with a single barrier: every thread sums the wave
+// totals below its wave itself (broadcast LDS reads). The caller must pass
+// another barrier before `sh` is written again.
+template <int NT, typename T>
+__device__ __forceinline__ T block_excl_scan_1b(T v, T* sh) {
+  constexpr int NW = NT / 64;
+  const uint32_t wave = threadIdx.x >> 6;
+  const T inc = wave_incl_scan(v);
+  if (lane_id() == 63) sh[wave] = inc;
+  lds_barrier();
+  T run = 0;
+#pragma unroll
+  for (int w = 0; w < NW - 1; w++) run += (uint32_t)w < wave ? sh[w] : (T)0;
+  return inc - v + run;
+}
+
 // Peer mask of a lane's digit: the lanes of the wave whose digit equals it
 // (and that are valid), one ballot per digit bit. Per bit: x = 0 / ~0 from
 // the lane's bit (v_bfe_i32), m = ballot, peers &= ~(m ^ x) (v_bitop3 on
@@ -860,16 +876,20 @@ __device__ __forceinline__ void scatter_process_tile(
   STAMP_DECL
   STAMP();
 
-  lds_barrier();  // the previous tile's readers of L are done
-  for (uint32_t i = threadIdx.x; i < (uint32_t)(NW * kMaxBins / 4); i += NT)
-    ((uint64_t*)&L.wc[0][0])[i] = 0;
+  if constexpr (LUT) lds_barrier();  // publishes the staged digit table
+  // each wave zeroes its own counter row (no barrier: a wave's LDS accesses
+  // execute in order, and the rank touches only the wave's row), so a wave
+  // starts ranking as soon as its own loads have landed
+  static_assert(kMaxBins % 256 == 0, "row zeroing: 64 lanes x u64");
+#pragma unroll
+  for (int i = 0; i < kMaxBins / 256; i++)
+    ((uint64_t*)&L.wc[wave][0])[i * 64 + lane_id()] = 0;
   auto valid = [&](int k) -> bool { return ebase + k * 64 < cnt; };
   // each key's digit, computed once (transform + digit cost ~15 VALU per key)
   uint32_t dg[IT];
 #pragma unroll
   for (int k = 0; k < IT; k++) dg[k] = pass_digit<LUT>(xf((U)(v0[k] & kmask)), P.shift, mask, lut);
   STAMP();  // 1: loads returned
-  lds_barrier();  // wc zeroed
 
   uint32_t pos[IT];
   // digits are < 2^kMaxDigitBits: every ballot unconditionally (no per-bit
@@ -890,8 +910,7 @@ __device__ __forceinline__ void scatter_process_tile(
         tb += c;
       }
     }
-    uint32_t tot;
-    const uint32_t ex = block_excl_scan_lds<NT>(tb, L.scan_sh, &tot);
+    const uint32_t ex = block_excl_scan_1b<NT>(tb, L.scan_sh);
     if (my_bin < nb) {
       L.bin_start[my_bin] = ex;
       L.gdst[my_bin] = P.start + my_off - (int64_t)ex;
