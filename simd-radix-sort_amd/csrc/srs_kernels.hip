@@ -309,15 +309,20 @@ __device__ __forceinline__ T block_excl_scan_lds(T v, T* sh, T* total) {
 // totals below its wave itself (broadcast LDS reads). The caller must pass
 // another barrier before `sh` is written again.
 template <int NT, typename T>
-__device__ __forceinline__ T block_excl_scan_1b(T v, T* sh) {
+__device__ __forceinline__ T block_excl_scan_1b(T v, T* sh, T* total = nullptr) {
   constexpr int NW = NT / 64;
   const uint32_t wave = threadIdx.x >> 6;
   const T inc = wave_incl_scan(v);
   if (lane_id() == 63) sh[wave] = inc;
   lds_barrier();
-  T run = 0;
+  T run = 0, all = 0;
 #pragma unroll
-  for (int w = 0; w < NW - 1; w++) run += (uint32_t)w < wave ? sh[w] : (T)0;
+  for (int w = 0; w < NW; w++) {
+    const T t = sh[w];
+    run += (uint32_t)w < wave ? t : (T)0;
+    all += t;
+  }
+  if (total) *total = all;
   return inc - v + run;
 }
 
@@ -1187,7 +1192,7 @@ __global__ __launch_bounds__(NT, WPE) void local_kernel(const SortDesc* __restri
           tsum += tb[q];
         }
         uint32_t tot;
-        uint32_t ex = block_excl_scan_lds<NT>(tsum, scan_sh, &tot);
+        uint32_t ex = block_excl_scan_1b<NT>(tsum, scan_sh, &tot);
 #pragma unroll
         for (int q = 0; q < BPT; q++) {
           const uint32_t b = threadIdx.x * BPT + q;
@@ -1228,7 +1233,7 @@ __global__ __launch_bounds__(NT, WPE) void local_kernel(const SortDesc* __restri
         tsum += tb[q] + tb[q + 1];
       }
       uint32_t tot;
-      uint32_t ex = block_excl_scan_lds<NT>(tsum, scan_sh, &tot);
+      uint32_t ex = block_excl_scan_1b<NT>(tsum, scan_sh, &tot);
       int mymax = 0;
 #pragma unroll
       for (int q = 0; q < BPT; q += 2) {
@@ -1343,7 +1348,9 @@ __global__ __launch_bounds__(NT, WPE) void local_kernel(const SortDesc* __restri
 #pragma unroll
     for (int k = 0; k < IT; k++) v[k] = c == 0 ? v0[k] : vn[k];
     if (c >= 1 && c + 1 < ncols) load_col(c + 1, vn);
-    lds_barrier();  // previous users of sbuf are done
+    // previous users of sbuf are done (for c == 0 the barrier after the perm
+    // writes already ordered every earlier sbuf access)
+    if (c > 0) lds_barrier();
 #pragma unroll
     for (int k = 0; k < IT; k++)
       if (valid(k)) sbuf[ebase + k * 64] = v[k];
