@@ -159,17 +159,37 @@ __device__ __forceinline__ void load_strip(uint64_t (&dst)[IT], const char* src,
   });
 }
 
+template <int W>
+__device__ __forceinline__ void bst(__amdgpu_buffer_rsrc_t r, uint64_t v, uint32_t voff,
+                                    uint32_t soff = 0) {
+  if constexpr (W == 1) __builtin_amdgcn_raw_buffer_store_b8((uint8_t)v, r, voff, soff, 0);
+  else if constexpr (W == 2) __builtin_amdgcn_raw_buffer_store_b16((uint16_t)v, r, voff, soff, 0);
+  else if constexpr (W == 4) __builtin_amdgcn_raw_buffer_store_b32((uint32_t)v, r, voff, soff, 0);
+  else {
+    typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+    u32x2 x;
+    x[0] = (uint32_t)v;
+    x[1] = (uint32_t)(v >> 32);
+    __builtin_amdgcn_raw_buffer_store_b64(x, r, voff, soff, 0);
+  }
+}
+
+// Stores slot k of a strip (the layout of load_strip). Range-checked buffer
+// stores: slots past cnt are dropped by the hardware, so value(k) must be
+// safe to evaluate for every k (the caller clamps its LDS indices).
 template <int IT, typename V>
 __device__ __forceinline__ void store_strip(char* out, uint32_t w, uint32_t st, int64_t first,
                                             int ebase, int cnt, V&& value) {
+  const __amdgpu_buffer_rsrc_t r =
+      strip_rsrc(out + first * (int64_t)st, cnt > 0 ? (uint32_t)cnt * st : 0u);
   with_strip<IT>(w, st, [&](auto W_, auto D_) {
     constexpr int W = decltype(W_)::value;
     constexpr bool D = decltype(D_)::value;
-    char* p0 = out + (first + ebase) * (int64_t)(D ? (uint32_t)W : st);
+    const uint32_t o0 = (uint32_t)ebase * (D ? (uint32_t)W : st);
 #pragma unroll
     for (int k = 0; k < IT; k++) {
-      const int64_t off = D ? (int64_t)k * 64 * W : (int64_t)k * 64 * st;
-      if (ebase + k * 64 < cnt) stw<W>(p0 + off, value(k));
+      if constexpr (D) bst<W>(r, value(k), o0 + (uint32_t)k * 64u * W);
+      else bst<W>(r, value(k), o0, __builtin_amdgcn_readfirstlane((uint32_t)k * 64u * st));
     }
   });
 }
@@ -1364,7 +1384,7 @@ __global__ __launch_bounds__(NT, WPE) void local_kernel(const SortDesc* __restri
   // output slot e takes input element perm[e]
   uint32_t id[IT];
 #pragma unroll
-  for (int k = 0; k < IT; k++) id[k] = perm[ebase + k * 64];
+  for (int k = 0; k < IT; k++) id[k] = valid(k) ? perm[ebase + k * 64] : 0u;  // store_strip reads every slot
 
   // ---- 4. columns: stage in input order, write in output order --------------
   // Software-pipelined: column c+1's loads are issued before column c is
