@@ -219,6 +219,7 @@ int get_ws(Workspace** out) {
 
 size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
+
 // ---------------------------------------------------------------------------
 // the sort driver (device pointers)
 // ---------------------------------------------------------------------------
@@ -371,7 +372,12 @@ int run_level(Workspace* W, int ks, const SortDesc* d_desc, LevelState& S, int f
   SRS_TRY(ensure(W->scan_tmp, scan_temp_elems(nbig) * 8));
   SegPlan* plan = (SegPlan*)W->plan.p;
   unsigned long long* var = (unsigned long long*)W->var.p;
-  {
+  const bool small_plan = nbig <= kPlanSmallMax;
+  if (small_plan) {
+    TimedScope ts("plan", (double)nbig, st);
+    launch_plan_small((Seg*)W->big[S.cur].p, nbig, plan, (int64_t*)W->tbase.p,
+                      (int64_t*)W->gbase.p, var, d_totals, &d_ctr->n_big, force_bits, st);
+  } else {
     TimedScope ts("plan", (double)nbig, st);
     HIP_TRY(hipMemsetAsync(d_totals + 3, 0, sizeof(uint64_t), st));
     launch_plan((Seg*)W->big[S.cur].p, nbig, plan, (int64_t*)W->tcount.p,
@@ -399,8 +405,8 @@ int run_level(Workspace* W, int ks, const SortDesc* d_desc, LevelState& S, int f
   SRS_TRY(ensure(W->gofs, (size_t)ngroups * kMaxBins * 8));
   int32_t* tile_seg = (int32_t*)W->tile_seg.p;
   int32_t* group_seg = (int32_t*)W->group_seg.p;
-  launch_seg_map((int64_t*)W->tbase.p, nbig, ntiles, tile_seg, st);
-  launch_seg_map((int64_t*)W->gbase.p, nbig, ngroups, group_seg, st);
+  launch_seg_map2((int64_t*)W->tbase.p, ntiles, tile_seg, (int64_t*)W->gbase.p, ngroups,
+                  group_seg, nbig, st);
   {
     TimedScope ts("count", (double)0, st);
     launch_count(ks, d_desc, plan, tile_seg, ntiles, (uint32_t*)W->hist.p, var, lut, st);
@@ -412,7 +418,8 @@ int run_level(Workspace* W, int ks, const SortDesc* d_desc, LevelState& S, int f
   SRS_TRY(ensure_keep(W->local, (S.n_local + worst) * sizeof(Seg), S.n_local * sizeof(Seg), st));
   SRS_TRY(ensure_keep(W->local2, (S.n_local2 + worst) * sizeof(Seg), S.n_local2 * sizeof(Seg), st));
   SRS_TRY(ensure_keep(W->copy, (S.n_copy + worst) * sizeof(Seg), S.n_copy * sizeof(Seg), st));
-  HIP_TRY(hipMemsetAsync(&d_ctr->n_big, 0, sizeof(unsigned long long), st));
+  if (!small_plan)  // (plan_small_kernel zeroed it)
+    HIP_TRY(hipMemsetAsync(&d_ctr->n_big, 0, sizeof(unsigned long long), st));
   {
     TimedScope ts("scan", (double)ntiles, st);
     launch_offsets(plan, nbig, group_seg, ngroups, (uint32_t*)W->hist.p,
@@ -502,9 +509,8 @@ int run_sort(Workspace* W, const Request& R, hipStream_t st) {
   }
   SRS_TRY(ensure(W->desc, sizeof(SortDesc)));
   SortDesc* d_desc = (SortDesc*)W->desc.p;
-  launch_set_desc(d, d_desc, st);
 
-  // ---- initial segments ----------------------------------------------------
+  // ---- initial segments (the descriptor is written with them) --------------
   const int home = inplace ? BUF_OUT : BUF_IN;
   SRS_TRY(ensure(W->big[0], 1024 * sizeof(Seg)));
   SRS_TRY(ensure(W->big[1], 1024 * sizeof(Seg)));
@@ -542,6 +548,7 @@ int run_sort(Workspace* W, const Request& R, hipStream_t st) {
     if (!hl2.empty())
       HIP_TRY(hipMemcpyAsync(W->local2.p, hl2.data(), hl2.size() * sizeof(Seg),
                              hipMemcpyHostToDevice, st));
+    launch_set_desc(d, d_desc, st);
     ListCounters c;
     memset(&c, 0, sizeof c);
     c.n_big = hb.size();
@@ -557,8 +564,8 @@ int run_sort(Workspace* W, const Request& R, hipStream_t st) {
   } else {
     Seg seg0{0, n, d.key_bits, home};
     const bool to_local = n <= kLocalCap;
-    launch_init_lists(seg0, to_local ? 1 : 0, (Seg*)W->big[0].p, (Seg*)W->local.p,
-                      (Seg*)W->local2.p, d_ctr, st);
+    launch_start(d, d_desc, seg0, to_local ? 1 : 0, (Seg*)W->big[0].p, (Seg*)W->local.p,
+                 (Seg*)W->local2.p, d_ctr, st);
     n_big = to_local ? 0 : 1;
     n_local = (to_local && n <= kLocalCapSmall) ? 1 : 0;
     n_local2 = (to_local && n > kLocalCapSmall) ? 1 : 0;
@@ -670,7 +677,6 @@ int run_partition(Workspace* W, const Request& R, int bits, const int32_t* d_lut
   d.lut_bits = bits;
   SRS_TRY(ensure(W->desc, sizeof(SortDesc)));
   SortDesc* d_desc = (SortDesc*)W->desc.p;
-  launch_set_desc(d, d_desc, st);
   SRS_TRY(ensure(W->big[0], 1024 * sizeof(Seg)));
   SRS_TRY(ensure(W->big[1], 1024 * sizeof(Seg)));
   SRS_TRY(ensure(W->local, 1024 * sizeof(Seg)));
@@ -679,8 +685,8 @@ int run_partition(Workspace* W, const Request& R, int bits, const int32_t* d_lut
   SRS_TRY(ensure(W->ctr, sizeof(ListCounters)));
   SRS_TRY(ensure(W->totals, 4 * sizeof(uint64_t)));
   Seg seg0{0, n, d.key_bits, BUF_IN};
-  launch_init_lists(seg0, 0, (Seg*)W->big[0].p, (Seg*)W->local.p, (Seg*)W->local2.p,
-                    (ListCounters*)W->ctr.p, st);
+  launch_start(d, d_desc, seg0, 0, (Seg*)W->big[0].p, (Seg*)W->local.p, (Seg*)W->local2.p,
+               (ListCounters*)W->ctr.p, st);
   int fb = 1;
   while ((1 << fb) < nparts) fb++;
   LevelState S{1, 0, 0, 0, 0};

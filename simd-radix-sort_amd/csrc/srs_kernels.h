@@ -11,10 +11,17 @@ namespace srs {
 void launch_plan(const Seg* big, int64_t nbig, SegPlan* plan, int64_t* tcount,
                  int64_t* gcount, unsigned long long* var_or, uint64_t* elems, int force_bits,
                  hipStream_t st);
+void launch_plan_small(const Seg* big, int64_t nbig, SegPlan* plan, int64_t* tbase,
+                       int64_t* gbase, unsigned long long* var_or, uint64_t* totals,
+                       unsigned long long* n_big_next, int force_bits, hipStream_t st);
+constexpr int64_t kPlanSmallMax = 16384;  // plan_small_kernel: one workgroup loops over these
+void launch_seg_map2(const int64_t* tbase, int64_t ntiles, int32_t* tile_seg,
+                     const int64_t* gbase, int64_t ngroups, int32_t* group_seg, int64_t nbig,
+                     hipStream_t st);
+void launch_start(const SortDesc& d, SortDesc* out, Seg seg0, int to_local, Seg* big, Seg* local,
+                  Seg* local2, ListCounters* ctr, hipStream_t st);
 void launch_plan_bases(SegPlan* plan, int64_t nbig, const int64_t* tbase,
                        const int64_t* gbase, hipStream_t st);
-void launch_seg_map(const int64_t* bases, int64_t nbig, int64_t n, int32_t* out,
-                    hipStream_t st);
 void launch_count(int key_size, const SortDesc* d, const SegPlan* plan,
                   const int32_t* tile_seg, int64_t ntiles, uint32_t* hist,
                   unsigned long long* var_or, bool lut, hipStream_t st);
@@ -44,7 +51,5 @@ void launch_sample_hist16(const void* keys, int key_bytes, int64_t n, int64_t st
 void launch_fill(int64_t n, int kind, uint64_t seed, uint64_t first, void* keys,
                  int npay, const Col* pays, hipStream_t st);
 void launch_set_desc(const SortDesc& d, SortDesc* out, hipStream_t st);
-void launch_init_lists(Seg seg0, int to_local, Seg* big, Seg* local, Seg* local2,
-                       ListCounters* ctr, hipStream_t st);
 
 }  // namespace srs

@@ -466,15 +466,7 @@ __device__ __forceinline__ int choose_bits(int64_t len, int rbits) {
   return bits;
 }
 
-__global__ void plan_kernel(const Seg* __restrict__ big, int64_t nbig,
-                            SegPlan* __restrict__ plan, int64_t* __restrict__ tcount,
-                            int64_t* __restrict__ gcount,
-                            unsigned long long* __restrict__ var_or,
-                            uint64_t* __restrict__ elems, int force_bits) {
-  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (s >= nbig) return;
-  const Seg g = big[s];
-  atomicAdd((unsigned long long*)elems, (unsigned long long)g.len);
+__device__ __forceinline__ SegPlan make_plan(const Seg& g, int force_bits) {
   SegPlan p;
   p.start = g.start;
   p.len = g.len;
@@ -487,10 +479,72 @@ __global__ void plan_kernel(const Seg* __restrict__ big, int64_t nbig,
   p.skip = 0;
   p.tile_base = 0;
   p.group_base = 0;
+  return p;
+}
+
+__global__ void plan_kernel(const Seg* __restrict__ big, int64_t nbig,
+                            SegPlan* __restrict__ plan, int64_t* __restrict__ tcount,
+                            int64_t* __restrict__ gcount,
+                            unsigned long long* __restrict__ var_or,
+                            uint64_t* __restrict__ elems, int force_bits) {
+  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= nbig) return;
+  const Seg g = big[s];
+  atomicAdd((unsigned long long*)elems, (unsigned long long)g.len);
+  const SegPlan p = make_plan(g, force_bits);
   plan[s] = p;
   tcount[s] = p.ntiles;
   gcount[s] = p.ngroups;
   var_or[s] = 0;
+}
+
+// Few segments (nbig <= kPlanSmallMax): the whole plan step in one
+// workgroup, i.e. plan_kernel + both exclusive scans + plan_bases_kernel in
+// one launch (the step is launch-bound for small sorts). Writes
+// totals[0] = tiles, totals[1] = scan groups, totals[3] = keys, and zeroes
+// the big-list counter the level's seg_scan appends to (the host has read it).
+constexpr int kPlanSmallThreads = 1024;
+__global__ __launch_bounds__(kPlanSmallThreads) void plan_small_kernel(
+    const Seg* __restrict__ big, int64_t nbig, SegPlan* __restrict__ plan,
+    int64_t* __restrict__ tbase, int64_t* __restrict__ gbase,
+    unsigned long long* __restrict__ var_or, uint64_t* __restrict__ totals,
+    unsigned long long* __restrict__ n_big_next, int force_bits) {
+  constexpr int NT = kPlanSmallThreads;
+  __shared__ uint64_t sh[3][NT / 64 + 1];
+  uint64_t tc = 0, gc = 0, ec = 0;
+  for (int64_t s0 = 0; s0 < nbig; s0 += NT) {
+    const int64_t s = s0 + threadIdx.x;
+    SegPlan p{};
+    uint64_t nt = 0, ng = 0, len = 0;
+    if (s < nbig) {
+      const Seg g = big[s];
+      p = make_plan(g, force_bits);
+      nt = (uint64_t)p.ntiles;
+      ng = (uint64_t)p.ngroups;
+      len = (uint64_t)g.len;
+    }
+    uint64_t tt, gt, et;
+    const uint64_t tex = block_excl_scan<NT>(nt, sh[0], &tt);
+    const uint64_t gex = block_excl_scan<NT>(ng, sh[1], &gt);
+    block_excl_scan<NT>(len, sh[2], &et);
+    if (s < nbig) {
+      p.tile_base = (int64_t)(tc + tex);
+      p.group_base = (int64_t)(gc + gex);
+      plan[s] = p;
+      tbase[s] = p.tile_base;
+      gbase[s] = p.group_base;
+      var_or[s] = 0;
+    }
+    tc += tt;
+    gc += gt;
+    ec += et;
+  }
+  if (threadIdx.x == 0) {
+    totals[0] = tc;
+    totals[1] = gc;
+    totals[3] = ec;
+    *n_big_next = 0;
+  }
 }
 
 __global__ void plan_bases_kernel(SegPlan* __restrict__ plan, int64_t nbig,
@@ -502,11 +556,21 @@ __global__ void plan_bases_kernel(SegPlan* __restrict__ plan, int64_t nbig,
   plan[s].group_base = gbase[s];
 }
 
-// index -> segment (binary search over the segments' exclusive bases)
-__global__ void seg_map_kernel(const int64_t* __restrict__ bases, int64_t nbig, int64_t n,
-                               int32_t* __restrict__ out) {
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= n) return;
+// index -> segment (binary search over the segments' exclusive bases);
+// both maps of a level in one launch: threads [0, ntiles) map tiles,
+// [ntiles, ntiles + ngroups) map scan groups
+__global__ void seg_map2_kernel(const int64_t* __restrict__ tbase, int64_t ntiles,
+                                int32_t* __restrict__ tile_seg, const int64_t* __restrict__ gbase,
+                                int64_t ngroups, int32_t* __restrict__ group_seg, int64_t nbig) {
+  int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t* bases = tbase;
+  int32_t* out = tile_seg;
+  if (t >= ntiles) {
+    t -= ntiles;
+    if (t >= ngroups) return;
+    bases = gbase;
+    out = group_seg;
+  }
   int64_t lo = 0, hi = nbig - 1;
   while (lo < hi) {
     const int64_t mid = (lo + hi + 1) >> 1;
@@ -1438,6 +1502,7 @@ __global__ __launch_bounds__(NT) void local_stable_kernel(
   __shared__ uint64_t sbuf[CAP];
   __shared__ uint16_t wc_perm[WCP];       // ballot counters [NW][NB], then perm[CAP]
   __shared__ uint32_t bflag[NB];          // bucket holds differing keys
+  __shared__ uint16_t sorig[CAP];         // wide words: original index by slot
   __shared__ uint32_t bin_start[NB + 1];
   __shared__ uint32_t scan_sh[NW + 1];
   __shared__ unsigned long long sh_or;
@@ -1500,11 +1565,13 @@ with_width(w, [&](auto W_) {
     const int lo = __ffsll((long long)var) - 1;
     const int hi = 63 - __clzll((long long)var);
     exact = hi - lo + 1 <= kLocalStableTopBits;
-    // the sort word packs (key bits 0..hi, original index): needs hi+1+IDXB <= 64
-    if (hi + 1 + IDXB > 64) {
-      if (threadIdx.x == 0) fallback[atomicAdd(fallback_count, 1ull)] = g;
-      continue;
-    }
+    // The sort word packs (key bits 0..hi, original index) when that fits
+    // in 64 bits. Otherwise (wide: e.g. a whole small sort of 64-bit keys)
+    // the word is the key alone and ties break by slot: the bucket pass is
+    // stable, so slot order inside a bucket is input order; the original
+    // index goes to sorig.
+    const bool wide = hi + 1 + IDXB > 64;
+    const int dsh = wide ? 0 : IDXB;  // key bits start here in a word
     const int nbits = (hi - lo + 1) < kLocalStableTopBits ? (hi - lo + 1) : kLocalStableTopBits;
     const int sh = hi - nbits + 1;
     const uint32_t mask = (1u << nbits) - 1;
@@ -1546,8 +1613,14 @@ with_width(w, [&](auto W_) {
       if (valid(k)) {
         const uint32_t d = digit(k);
         const uint32_t p = bin_start[d] + wc_perm[wave * NB + d] + rank[k];
-        if (exact) sidx[p] = (uint16_t)(ebase + k * 64);
-        else sbuf[p] = (((uint64_t)ukey(k) & keep) << IDXB) | (uint64_t)(ebase + k * 64);
+        if (exact) {
+          sidx[p] = (uint16_t)(ebase + k * 64);
+        } else if (wide) {
+          sbuf[p] = (uint64_t)ukey(k) & keep;
+          sorig[p] = (uint16_t)(ebase + k * 64);
+        } else {
+          sbuf[p] = (((uint64_t)ukey(k) & keep) << IDXB) | (uint64_t)(ebase + k * 64);
+        }
       }
     }
     lds_barrier();
@@ -1558,8 +1631,8 @@ with_width(w, [&](auto W_) {
       const int p = i * NT + (int)threadIdx.x;
       if (p < cnt) {
         const uint64_t x = sbuf[p];
-        const uint32_t d = (uint32_t)(x >> (sh + IDXB)) & mask;
-        if (((x ^ sbuf[bin_start[d]]) >> IDXB) != 0) bflag[d] = 1;
+        const uint32_t d = (uint32_t)(x >> (sh + dsh)) & mask;
+        if (((x ^ sbuf[bin_start[d]]) >> dsh) != 0) bflag[d] = 1;
       }
     }
     lds_barrier();
@@ -1599,7 +1672,7 @@ with_width(w, [&](auto W_) {
         r[i] = 0;
         if (p < cnt) {
           x[i] = sbuf[p];
-          const uint32_t d = (uint32_t)(x[i] >> (sh + IDXB)) & mask;
+          const uint32_t d = (uint32_t)(x[i] >> (sh + dsh)) & mask;
           if (bflag[d]) {
             bs[i] = bin_start[d];
             bl[i] = bin_start[d + 1] - bs[i];
@@ -1612,15 +1685,30 @@ with_width(w, [&](auto W_) {
         const int t2 = __shfl_xor(wmax, o, 64);
         wmax = t2 > wmax ? t2 : wmax;
       }
-      for (int j = 0; j < wmax; j++) {
+      if (!wide) {
+        for (int j = 0; j < wmax; j++) {
 #pragma unroll
-        for (int i = 0; i < H; i++)
-          if ((uint32_t)j < bl[i]) r[i] += sbuf[bs[i] + j] < x[i];
+          for (int i = 0; i < H; i++)
+            if ((uint32_t)j < bl[i]) r[i] += sbuf[bs[i] + j] < x[i];
+        }
+      } else {
+        for (int j = 0; j < wmax; j++) {
+#pragma unroll
+          for (int i = 0; i < H; i++) {
+            const uint32_t q = bs[i] + (uint32_t)j;
+            const int p = (half * H + i) * NT + (int)threadIdx.x;
+            if ((uint32_t)j < bl[i]) {
+              const uint64_t w = sbuf[q];
+              r[i] += (w < x[i]) | ((w == x[i]) & ((int)q < p));
+            }
+          }
+        }
       }
 #pragma unroll
       for (int i = 0; i < H; i++) {
         const int p = (half * H + i) * NT + (int)threadIdx.x;
-        if (p < cnt) perm[bs[i] + r[i]] = (uint16_t)(x[i] & ((1u << IDXB) - 1));
+        if (p < cnt)
+          perm[bs[i] + r[i]] = wide ? sorig[p] : (uint16_t)(x[i] & ((1u << IDXB) - 1));
       }
     }
     lds_barrier();
@@ -1860,16 +1948,26 @@ void launch_plan(const Seg* big, int64_t nbig, SegPlan* plan, int64_t* tcount,
                                                               gcount, var_or, elems, force_bits);
 }
 
+void launch_plan_small(const Seg* big, int64_t nbig, SegPlan* plan, int64_t* tbase,
+                       int64_t* gbase, unsigned long long* var_or, uint64_t* totals,
+                       unsigned long long* n_big_next, int force_bits, hipStream_t st) {
+  plan_small_kernel<<<1, kPlanSmallThreads, 0, st>>>(big, nbig, plan, tbase, gbase, var_or,
+                                                     totals, n_big_next, force_bits);
+}
+
 void launch_plan_bases(SegPlan* plan, int64_t nbig, const int64_t* tbase,
                        const int64_t* gbase, hipStream_t st) {
   plan_bases_kernel<<<(unsigned)((nbig + 255) / 256), 256, 0, st>>>(plan, nbig, tbase,
                                                                     gbase);
 }
 
-void launch_seg_map(const int64_t* bases, int64_t nbig, int64_t n, int32_t* out,
-                    hipStream_t st) {
+void launch_seg_map2(const int64_t* tbase, int64_t ntiles, int32_t* tile_seg,
+                     const int64_t* gbase, int64_t ngroups, int32_t* group_seg, int64_t nbig,
+                     hipStream_t st) {
+  const int64_t n = ntiles + ngroups;
   if (n > 0)
-    seg_map_kernel<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(bases, nbig, n, out);
+    seg_map2_kernel<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(tbase, ntiles, tile_seg, gbase,
+                                                                 ngroups, group_seg, nbig);
 }
 
 void launch_count(int key_size, const SortDesc* d, const SegPlan* plan,
@@ -2004,8 +2102,8 @@ __global__ void set_desc_kernel(SortDesc d, SortDesc* out) {
   if (threadIdx.x == 0) *out = d;
 }
 
-__global__ void init_lists_kernel(Seg seg0, int to_local, Seg* big, Seg* local,
-                                  Seg* local2, ListCounters* ctr) {
+__device__ __forceinline__ void init_lists_body(Seg seg0, int to_local, Seg* big, Seg* local,
+                                                Seg* local2, ListCounters* ctr) {
   if (threadIdx.x == 0) {
     ctr->n_big = to_local ? 0 : 1;
     const bool small = seg0.len <= kLocalCapSmall;
@@ -2020,13 +2118,22 @@ __global__ void init_lists_kernel(Seg seg0, int to_local, Seg* big, Seg* local,
   }
 }
 
+
 void launch_set_desc(const SortDesc& d, SortDesc* out, hipStream_t st) {
   set_desc_kernel<<<1, 64, 0, st>>>(d, out);
 }
 
-void launch_init_lists(Seg seg0, int to_local, Seg* big, Seg* local, Seg* local2,
-                       ListCounters* ctr, hipStream_t st) {
-  init_lists_kernel<<<1, 64, 0, st>>>(seg0, to_local, big, local, local2, ctr);
+// set_desc + init_lists in one launch (a small sort is launch-bound)
+__global__ void start_kernel(SortDesc d, SortDesc* out, Seg seg0, int to_local, Seg* big,
+                             Seg* local, Seg* local2, ListCounters* ctr) {
+  if (threadIdx.x == 0) *out = d;
+  init_lists_body(seg0, to_local, big, local, local2, ctr);
 }
+
+void launch_start(const SortDesc& d, SortDesc* out, Seg seg0, int to_local, Seg* big, Seg* local,
+                  Seg* local2, ListCounters* ctr, hipStream_t st) {
+  start_kernel<<<1, 64, 0, st>>>(d, out, seg0, to_local, big, local, local2, ctr);
+}
+
 
 }  // namespace srs

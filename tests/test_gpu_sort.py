@@ -168,6 +168,52 @@ def test_sizes_u64_vs_oracle(n):
     assert bytes_equal(k, ok) and bytes_equal(p, op)
 
 
+def _fallback_keys(case, n, rng):
+    if case == "random64":  # full 64-bit range: too wide for packed words -> stable (wide words)
+        return rng.integers(0, 1 << 64, n, dtype=np.uint64)
+    if case == "dups":      # big all-equal buckets: fast kernel -> stable kernel
+        k = np.full(n, 0x1234_5678_9ABC, dtype=np.uint64)
+        m = rng.random(n) < 0.1
+        k[m] = rng.integers(1 << 62, 1 << 63, int(m.sum()), dtype=np.uint64)  # never in its bucket
+    elif case == "wide":    # a big mixed bucket and a 61-bit varying range: -> stable -> LSD
+        k = rng.integers(0, 1 << 20, n, dtype=np.uint64)
+        k[rng.choice(n, 5, replace=False)] = rng.integers(1 << 59, 1 << 61, 5, dtype=np.uint64)
+    else:                   # "groups": the same inside every top-6-bit group, many segments
+        k = rng.integers(0, 1 << 16, n, dtype=np.uint64) | (
+            (np.arange(n, dtype=np.uint64) % np.uint64(64)) << np.uint64(58))
+        m = rng.random(n) < 0.002
+        k[m] |= rng.integers(1 << 40, 1 << 57, int(m.sum()), dtype=np.uint64)
+    return k
+
+
+@pytest.mark.parametrize("case,n", [("random64", 16), ("random64", 3000), ("random64", 8000),
+                                    ("dups", 3000), ("dups", 8000), ("wide", 3000),
+                                    ("wide", 8000), ("groups", 300_000)])
+def test_local_fallback_paths(case, n):
+    """The stable and LSD local kernels run only when the fast kernel hands
+    segments over (the host reads the fallback counters first): these inputs
+    force each path; the result must equal a stable sort bit for bit."""
+    rng = np.random.default_rng(7)
+    keys = _fallback_keys(case, n, rng)
+    idx = np.arange(n, dtype=np.uint64)
+    k, p = keys.copy(), idx.copy()
+    srs_amd.set_kernel_timing(True)
+    srs_amd.reset_kernel_stats()
+    try:
+        srs_amd.sort(k, p)
+        stable_n = srs_amd.kernel_stats("local_stable")[2]
+        lsd_n = srs_amd.kernel_stats("local_lsd")[2]
+    finally:
+        srs_amd.set_kernel_timing(False)
+    order = np.argsort(keys, kind="stable")
+    assert bytes_equal(k, keys[order]) and bytes_equal(p, idx[order])
+    assert stable_n > 0, "stable fallback not exercised"
+    if case in ("wide", "groups"):
+        assert lsd_n > 0, "LSD fallback not exercised"
+    else:
+        assert lsd_n == 0, "the stable kernel should have finished these segments"
+
+
 @pytest.mark.parametrize("sizes", [[1], [2], [4], [8], [8, 1], [4, 4], [8, 8, 8], [1] * 63,
                                    [2, 8, 1, 4]])
 def test_payload_packs(sizes):
