@@ -400,7 +400,10 @@ int run_level(Workspace* W, int ks, const SortDesc* d_desc, LevelState& S, int f
   SRS_TRY(ensure(W->tile_seg, ntiles * 4));
   SRS_TRY(ensure(W->group_seg, ngroups * 4));
   SRS_TRY(ensure(W->hist, (size_t)ntiles * kMaxBins * 4));
-  SRS_TRY(ensure(W->offs, (size_t)ntiles * kMaxBins * 8));
+  // u32 tile offsets written over the histogram rows when every segment of
+  // the level is < 2^32 keys (all of them are when the level is)
+  const bool offs32 = W->h_totals[3] < (1ull << 32);
+  if (!offs32) SRS_TRY(ensure(W->offs, (size_t)ntiles * kMaxBins * 8));
   SRS_TRY(ensure(W->gsum, (size_t)ngroups * kMaxBins * 4));
   SRS_TRY(ensure(W->gofs, (size_t)ngroups * kMaxBins * 8));
   int32_t* tile_seg = (int32_t*)W->tile_seg.p;
@@ -424,12 +427,13 @@ int run_level(Workspace* W, int ks, const SortDesc* d_desc, LevelState& S, int f
     TimedScope ts("scan", (double)ntiles, st);
     launch_offsets(plan, nbig, group_seg, ngroups, (uint32_t*)W->hist.p,
                    (uint32_t*)W->gsum.p, (uint64_t*)W->gofs.p, (uint64_t*)W->sbase.p,
-                   (uint64_t*)W->offs.p, var, (Seg*)W->big[nxt].p, (Seg*)W->local.p,
+                   (uint64_t*)W->offs.p, offs32, var, (Seg*)W->big[nxt].p, (Seg*)W->local.p,
                    (Seg*)W->local2.p, (Seg*)W->copy.p, d_ctr, lut_rbits, st);
   }
   {
     TimedScope ts("scatter", (double)0, st);
-    launch_scatter(ks, d_desc, plan, tile_seg, (uint64_t*)W->offs.p, ntiles, lut, st);
+    launch_scatter(ks, d_desc, plan, tile_seg, (uint64_t*)W->offs.p,
+                   offs32 ? (const uint32_t*)W->hist.p : nullptr, ntiles, lut, st);
   }
   HIP_TRY(hipMemcpyAsync(W->h_ctr, d_ctr, sizeof(ListCounters), hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));

@@ -30,12 +30,12 @@ void launch_excl_scan(const uint64_t* x, uint64_t* y, int64_t n, uint64_t* temp,
                       uint64_t* total, hipStream_t st);
 void launch_offsets(SegPlan* plan, int64_t nbig, const int32_t* group_seg, int64_t ngroups,
                     const uint32_t* hist, uint32_t* gsum, uint64_t* gofs, uint64_t* sbase,
-                    uint64_t* offs, const unsigned long long* var_or, Seg* big_next,
-                    Seg* local, Seg* local2, Seg* copy, ListCounters* ctr,
+                    uint64_t* offs, bool offs_in_hist, const unsigned long long* var_or,
+                    Seg* big_next, Seg* local, Seg* local2, Seg* copy, ListCounters* ctr,
                     const int32_t* lut_rbits, hipStream_t st);
 void launch_scatter(int key_size, const SortDesc* d, const SegPlan* plan,
-                    const int32_t* tile_seg, const uint64_t* offs, int64_t ntiles, bool lut,
-                    hipStream_t st);
+                    const int32_t* tile_seg, const uint64_t* offs, const uint32_t* offs32,
+                    int64_t ntiles, bool lut, hipStream_t st);
 void launch_key_hist(int key_size, int64_t n, const void* keys, const SortDesc& d, int bits,
                      unsigned long long* hist, hipStream_t st);
 void launch_local(int key_size, const SortDesc* d, const Seg* segs, int64_t nsegs, int big_class,

@@ -894,10 +894,15 @@ __global__ __launch_bounds__(kMaxBins) void seg_scan_kernel(
 }
 
 // Per group: turn group offsets into every tile's bucket offsets.
+// Tile offsets (bucket start of each tile inside its segment). offs32 != 0
+// (every segment of the level < 2^32 keys): u32 offsets written over the
+// tile's own histogram row (each thread reads its count before writing that
+// slot), half the bytes of the u64 rows in `offs` for this kernel and the
+// scatter that reads them.
 __global__ __launch_bounds__(kMaxBins) void tile_offs_kernel(
     const SegPlan* __restrict__ plan, const int32_t* __restrict__ group_seg,
-    const uint32_t* __restrict__ hist, const uint64_t* __restrict__ gofs,
-    const uint64_t* __restrict__ sbase, uint64_t* __restrict__ offs) {
+    const uint32_t* hist, const uint64_t* __restrict__ gofs,
+    const uint64_t* __restrict__ sbase, uint64_t* __restrict__ offs, uint32_t* offs32) {
   const int64_t g = blockIdx.x;
   const int32_t s = group_seg[g];
   const SegPlan P = plan[s];
@@ -906,20 +911,26 @@ __global__ __launch_bounds__(kMaxBins) void tile_offs_kernel(
   const int64_t t0 = P.tile_base + (g - P.group_base) * kScanGroup;
   const int64_t t1 = min(t0 + kScanGroup, P.tile_base + P.ntiles);
   uint64_t run = sbase[s * kMaxBins + b] + gofs[g * kMaxBins + b];
-  int64_t t = t0;
-  for (; t + 4 <= t1; t += 4) {
-    const uint32_t a0 = hist[(t + 0) * kMaxBins + b], a1 = hist[(t + 1) * kMaxBins + b];
-    const uint32_t a2 = hist[(t + 2) * kMaxBins + b], a3 = hist[(t + 3) * kMaxBins + b];
-    offs[(t + 0) * kMaxBins + b] = run;
-    offs[(t + 1) * kMaxBins + b] = run + a0;
-    offs[(t + 2) * kMaxBins + b] = run + a0 + a1;
-    offs[(t + 3) * kMaxBins + b] = run + a0 + a1 + a2;
-    run += (uint64_t)a0 + a1 + a2 + a3;
-  }
-  for (; t < t1; t++) {
-    offs[t * kMaxBins + b] = run;
-    run += hist[t * kMaxBins + b];
-  }
+  auto body = [&](auto* out) {
+    using O = std::remove_pointer_t<decltype(out)>;
+    int64_t t = t0;
+    for (; t + 4 <= t1; t += 4) {
+      const uint32_t a0 = hist[(t + 0) * kMaxBins + b], a1 = hist[(t + 1) * kMaxBins + b];
+      const uint32_t a2 = hist[(t + 2) * kMaxBins + b], a3 = hist[(t + 3) * kMaxBins + b];
+      out[(t + 0) * kMaxBins + b] = (O)run;
+      out[(t + 1) * kMaxBins + b] = (O)(run + a0);
+      out[(t + 2) * kMaxBins + b] = (O)(run + a0 + a1);
+      out[(t + 3) * kMaxBins + b] = (O)(run + a0 + a1 + a2);
+      run += (uint64_t)a0 + a1 + a2 + a3;
+    }
+    for (; t < t1; t++) {
+      const uint32_t a = hist[t * kMaxBins + b];
+      out[t * kMaxBins + b] = (O)run;
+      run += a;
+    }
+  };
+  if (offs32) body(offs32);
+  else body(offs);
 }
 
 // ---------------------------------------------------------------------------
@@ -957,8 +968,9 @@ struct TileInfo {
 template <typename KT, typename U>
 __device__ __forceinline__ TileInfo scatter_load_tile(
     const SortDesc* __restrict__ desc, const SegPlan* __restrict__ plan,
-    const int32_t* __restrict__ tile_seg, const uint64_t* __restrict__ offs, int64_t t,
-    int ncols, uint64_t (&v0)[kScatterItems], uint64_t (&v1)[kScatterItems], int64_t& my_off) {
+    const int32_t* __restrict__ tile_seg, const uint64_t* __restrict__ offs,
+    const uint32_t* __restrict__ offs32, int64_t t, int ncols, uint64_t (&v0)[kScatterItems],
+    uint64_t (&v1)[kScatterItems], int64_t& my_off) {
   constexpr int IT = kScatterItems;
   TileInfo ti;
   ti.s = tile_seg[t];
@@ -974,7 +986,9 @@ __device__ __forceinline__ TileInfo scatter_load_tile(
     load_strip<IT>(v1, desc->cols[1].base[P.buf], desc->cols[1].width, desc->cols[1].stride,
                    ti.base, ebase, ti.cnt);
   my_off = 0;
-  if (ti.cnt > 0 && threadIdx.x < (1u << P.bits)) my_off = (int64_t)offs[t * kMaxBins + threadIdx.x];
+  if (ti.cnt > 0 && threadIdx.x < (1u << P.bits))
+    my_off = offs32 ? (int64_t)offs32[t * kMaxBins + threadIdx.x]
+                    : (int64_t)offs[t * kMaxBins + threadIdx.x];
   return ti;
 }
 
@@ -1107,14 +1121,16 @@ __device__ __forceinline__ void scatter_process_tile(
 template <typename KT, typename U, bool LUT, bool CZ>
 __global__ __launch_bounds__(kScatterThreads, SRS_SCATTER_WAVES_PER_EU) void scatter_kernel(
     const SortDesc* __restrict__ desc, const SegPlan* __restrict__ plan,
-    const int32_t* __restrict__ tile_seg, const uint64_t* __restrict__ offs) {
+    const int32_t* __restrict__ tile_seg, const uint64_t* __restrict__ offs,
+    const uint32_t* __restrict__ offs32) {
   __shared__ ScatterLds<LUT> L;
   __shared__ uint16_t slut[LUT ? kLdsLutEntries : 1];
   const int64_t t = xcd_remap(blockIdx.x, gridDim.x);
   const int ncols = desc->ncols;
   uint64_t v0[kScatterItems], v1[kScatterItems];
   int64_t my_off;
-  const TileInfo ti = scatter_load_tile<KT, U>(desc, plan, tile_seg, offs, t, ncols, v0, v1, my_off);
+  const TileInfo ti =
+      scatter_load_tile<KT, U>(desc, plan, tile_seg, offs, offs32, t, ncols, v0, v1, my_off);
   if (ti.cnt == 0) return;
   // (the table is published by the barrier at the top of the tile)
   const DigitLut lut = stage_lut<LUT, kScatterThreads>(desc, slut);
@@ -1996,27 +2012,28 @@ void launch_excl_scan(const uint64_t* x, uint64_t* y, int64_t n, uint64_t* temp,
 
 void launch_offsets(SegPlan* plan, int64_t nbig, const int32_t* group_seg, int64_t ngroups,
                     const uint32_t* hist, uint32_t* gsum, uint64_t* gofs, uint64_t* sbase,
-                    uint64_t* offs, const unsigned long long* var_or, Seg* big_next,
+                    uint64_t* offs, bool offs_in_hist, const unsigned long long* var_or,
+                    Seg* big_next,
                     Seg* local, Seg* local2, Seg* copy, ListCounters* ctr,
                     const int32_t* lut_rbits, hipStream_t st) {
   group_sum_kernel<<<(unsigned)ngroups, kMaxBins, 0, st>>>(plan, group_seg, hist, gsum);
   seg_scan_kernel<<<(unsigned)nbig, kMaxBins, 0, st>>>(plan, gsum, gofs, sbase, var_or,
                                                       big_next, local, local2, copy, ctr,
                                                       lut_rbits);
-  tile_offs_kernel<<<(unsigned)ngroups, kMaxBins, 0, st>>>(plan, group_seg, hist, gofs, sbase,
-                                                          offs);
+  tile_offs_kernel<<<(unsigned)ngroups, kMaxBins, 0, st>>>(
+      plan, group_seg, hist, gofs, sbase, offs, offs_in_hist ? const_cast<uint32_t*>(hist) : nullptr);
 }
 
 void launch_scatter(int key_size, const SortDesc* d, const SegPlan* plan,
-                    const int32_t* tile_seg, const uint64_t* offs, int64_t ntiles, bool lut,
-                    hipStream_t st) {
+                    const int32_t* tile_seg, const uint64_t* offs, const uint32_t* offs32,
+                    int64_t ntiles, bool lut, hipStream_t st) {
 #define CALL(KT, U, CZ)                                                                 \
   if (lut)                                                                              \
     scatter_kernel<KT, U, true, CZ><<<(unsigned)ntiles, kScatterThreads, 0, st>>>(        \
-        d, plan, tile_seg, offs);                                                       \
+        d, plan, tile_seg, offs, offs32);                                               \
   else                                                                                  \
     scatter_kernel<KT, U, false, CZ><<<(unsigned)ntiles, kScatterThreads, 0, st>>>(       \
-        d, plan, tile_seg, offs)
+        d, plan, tile_seg, offs, offs32)
   SRS_KEY_DISPATCH(key_size, CALL)
 #undef CALL
 }
