@@ -399,11 +399,11 @@ int run_level(Workspace* W, int ks, const SortDesc* d_desc, LevelState& S, int f
 
   SRS_TRY(ensure(W->tile_seg, ntiles * 4));
   SRS_TRY(ensure(W->group_seg, ngroups * 4));
-  SRS_TRY(ensure(W->hist, (size_t)ntiles * kMaxBins * 4));
-  // u32 tile offsets written over the histogram rows when every segment of
-  // the level is < 2^32 keys (all of them are when the level is)
+  SRS_TRY(ensure(W->hist, (size_t)ntiles * kMaxBins * 2));
+  // u16 tile counts; u32 tile offsets when every segment of the level is
+  // < 2^32 keys (all of them are when the level is), else u64
   const bool offs32 = W->h_totals[3] < (1ull << 32);
-  if (!offs32) SRS_TRY(ensure(W->offs, (size_t)ntiles * kMaxBins * 8));
+  SRS_TRY(ensure(W->offs, (size_t)ntiles * kMaxBins * (offs32 ? 4 : 8)));
   SRS_TRY(ensure(W->gsum, (size_t)ngroups * kMaxBins * 4));
   SRS_TRY(ensure(W->gofs, (size_t)ngroups * kMaxBins * 8));
   int32_t* tile_seg = (int32_t*)W->tile_seg.p;
@@ -412,7 +412,7 @@ int run_level(Workspace* W, int ks, const SortDesc* d_desc, LevelState& S, int f
                   group_seg, nbig, st);
   {
     TimedScope ts("count", (double)0, st);
-    launch_count(ks, d_desc, plan, tile_seg, ntiles, (uint32_t*)W->hist.p, var, lut, st);
+    launch_count(ks, d_desc, plan, tile_seg, ntiles, (uint16_t*)W->hist.p, var, lut, st);
   }
   // ---- offsets + children (list capacity for the worst case: every bin non-empty)
   const size_t worst = (size_t)nbig * kMaxBins;
@@ -425,15 +425,16 @@ int run_level(Workspace* W, int ks, const SortDesc* d_desc, LevelState& S, int f
     HIP_TRY(hipMemsetAsync(&d_ctr->n_big, 0, sizeof(unsigned long long), st));
   {
     TimedScope ts("scan", (double)ntiles, st);
-    launch_offsets(plan, nbig, group_seg, ngroups, (uint32_t*)W->hist.p,
+    launch_offsets(plan, nbig, group_seg, ngroups, (uint16_t*)W->hist.p,
                    (uint32_t*)W->gsum.p, (uint64_t*)W->gofs.p, (uint64_t*)W->sbase.p,
-                   (uint64_t*)W->offs.p, offs32, var, (Seg*)W->big[nxt].p, (Seg*)W->local.p,
+                   offs32 ? nullptr : (uint64_t*)W->offs.p, offs32 ? (uint32_t*)W->offs.p : nullptr,
+                   var, (Seg*)W->big[nxt].p, (Seg*)W->local.p,
                    (Seg*)W->local2.p, (Seg*)W->copy.p, d_ctr, lut_rbits, st);
   }
   {
     TimedScope ts("scatter", (double)0, st);
     launch_scatter(ks, d_desc, plan, tile_seg, (uint64_t*)W->offs.p,
-                   offs32 ? (const uint32_t*)W->hist.p : nullptr, ntiles, lut, st);
+                   offs32 ? (const uint32_t*)W->offs.p : nullptr, ntiles, lut, st);
   }
   HIP_TRY(hipMemcpyAsync(W->h_ctr, d_ctr, sizeof(ListCounters), hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));

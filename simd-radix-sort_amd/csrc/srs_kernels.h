@@ -23,14 +23,14 @@ void launch_start(const SortDesc& d, SortDesc* out, Seg seg0, int to_local, Seg*
 void launch_plan_bases(SegPlan* plan, int64_t nbig, const int64_t* tbase,
                        const int64_t* gbase, hipStream_t st);
 void launch_count(int key_size, const SortDesc* d, const SegPlan* plan,
-                  const int32_t* tile_seg, int64_t ntiles, uint32_t* hist,
+                  const int32_t* tile_seg, int64_t ntiles, uint16_t* hist,
                   unsigned long long* var_or, bool lut, hipStream_t st);
 int64_t scan_temp_elems(int64_t n);
 void launch_excl_scan(const uint64_t* x, uint64_t* y, int64_t n, uint64_t* temp,
                       uint64_t* total, hipStream_t st);
 void launch_offsets(SegPlan* plan, int64_t nbig, const int32_t* group_seg, int64_t ngroups,
-                    const uint32_t* hist, uint32_t* gsum, uint64_t* gofs, uint64_t* sbase,
-                    uint64_t* offs, bool offs_in_hist, const unsigned long long* var_or,
+                    const uint16_t* hist, uint32_t* gsum, uint64_t* gofs, uint64_t* sbase,
+                    uint64_t* offs, uint32_t* offs32, const unsigned long long* var_or,
                     Seg* big_next, Seg* local, Seg* local2, Seg* copy, ListCounters* ctr,
                     const int32_t* lut_rbits, hipStream_t st);
 void launch_scatter(int key_size, const SortDesc* d, const SegPlan* plan,

@@ -622,7 +622,7 @@ __device__ __forceinline__ DigitLut stage_lut(const SortDesc* desc, uint16_t* sl
 template <typename KT, typename U, bool LUT, bool CZ>
 __global__ __launch_bounds__(kCountThreads) void count_kernel(
     const SortDesc* __restrict__ desc, const SegPlan* __restrict__ plan,
-    const int32_t* __restrict__ tile_seg, uint32_t* __restrict__ hist,
+    const int32_t* __restrict__ tile_seg, uint16_t* __restrict__ hist,
     unsigned long long* __restrict__ var_or) {
   __shared__ uint32_t h[kMaxBins];
   __shared__ unsigned long long sh_or;
@@ -665,9 +665,12 @@ __global__ __launch_bounds__(kCountThreads) void count_kernel(
   }
   if (vor) atomicOr(&sh_or, (unsigned long long)vor);
   __syncthreads();
-  // tile-major row: one coalesced 4*nb-byte write per tile
-  uint32_t* row = hist + t * kMaxBins;
-  for (uint32_t i = threadIdx.x; i < nb; i += kCountThreads) row[i] = h[i];
+  // tile-major row of u16 counts (a tile holds <= kTile = 4096 keys): one
+  // coalesced 2*nb-byte write per tile, written as packed pairs
+  static_assert(kTile < 65536, "u16 tile counts");
+  uint32_t* row = (uint32_t*)(hist + t * kMaxBins);
+  for (uint32_t i = threadIdx.x; i < nb / 2; i += kCountThreads)
+    row[i] = h[2 * i] | (h[2 * i + 1] << 16);
   if (threadIdx.x == 0 && sh_or) {
     // most tiles add no new bits: skip the (contended) atomic then
     const unsigned long long known =
@@ -683,7 +686,7 @@ __global__ __launch_bounds__(kCountThreads) void count_kernel(
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(kMaxBins) void group_sum_kernel(
     const SegPlan* __restrict__ plan, const int32_t* __restrict__ group_seg,
-    const uint32_t* __restrict__ hist, uint32_t* __restrict__ gsum) {
+    const uint16_t* __restrict__ hist, uint32_t* __restrict__ gsum) {
   const int64_t g = blockIdx.x;
   const SegPlan P = plan[group_seg[g]];
   const uint32_t b = threadIdx.x;
@@ -895,14 +898,13 @@ __global__ __launch_bounds__(kMaxBins) void seg_scan_kernel(
 
 // Per group: turn group offsets into every tile's bucket offsets.
 // Tile offsets (bucket start of each tile inside its segment). offs32 != 0
-// (every segment of the level < 2^32 keys): u32 offsets written over the
-// tile's own histogram row (each thread reads its count before writing that
-// slot), half the bytes of the u64 rows in `offs` for this kernel and the
-// scatter that reads them.
+// (every segment of the level < 2^32 keys): u32 rows, half the bytes of the
+// u64 rows in `offs` for this kernel and the scatter that reads them.
 __global__ __launch_bounds__(kMaxBins) void tile_offs_kernel(
     const SegPlan* __restrict__ plan, const int32_t* __restrict__ group_seg,
-    const uint32_t* hist, const uint64_t* __restrict__ gofs,
-    const uint64_t* __restrict__ sbase, uint64_t* __restrict__ offs, uint32_t* offs32) {
+    const uint16_t* __restrict__ hist, const uint64_t* __restrict__ gofs,
+    const uint64_t* __restrict__ sbase, uint64_t* __restrict__ offs,
+    uint32_t* __restrict__ offs32) {
   const int64_t g = blockIdx.x;
   const int32_t s = group_seg[g];
   const SegPlan P = plan[s];
@@ -1987,7 +1989,7 @@ void launch_seg_map2(const int64_t* tbase, int64_t ntiles, int32_t* tile_seg,
 }
 
 void launch_count(int key_size, const SortDesc* d, const SegPlan* plan,
-                  const int32_t* tile_seg, int64_t ntiles, uint32_t* hist,
+                  const int32_t* tile_seg, int64_t ntiles, uint16_t* hist,
                   unsigned long long* var_or, bool lut, hipStream_t st) {
 #define CALL(KT, U, CZ)                                                                 \
   if (lut)                                                                              \
@@ -2011,8 +2013,8 @@ void launch_excl_scan(const uint64_t* x, uint64_t* y, int64_t n, uint64_t* temp,
 }
 
 void launch_offsets(SegPlan* plan, int64_t nbig, const int32_t* group_seg, int64_t ngroups,
-                    const uint32_t* hist, uint32_t* gsum, uint64_t* gofs, uint64_t* sbase,
-                    uint64_t* offs, bool offs_in_hist, const unsigned long long* var_or,
+                    const uint16_t* hist, uint32_t* gsum, uint64_t* gofs, uint64_t* sbase,
+                    uint64_t* offs, uint32_t* offs32, const unsigned long long* var_or,
                     Seg* big_next,
                     Seg* local, Seg* local2, Seg* copy, ListCounters* ctr,
                     const int32_t* lut_rbits, hipStream_t st) {
@@ -2021,7 +2023,7 @@ void launch_offsets(SegPlan* plan, int64_t nbig, const int32_t* group_seg, int64
                                                       big_next, local, local2, copy, ctr,
                                                       lut_rbits);
   tile_offs_kernel<<<(unsigned)ngroups, kMaxBins, 0, st>>>(
-      plan, group_seg, hist, gofs, sbase, offs, offs_in_hist ? const_cast<uint32_t*>(hist) : nullptr);
+      plan, group_seg, hist, gofs, sbase, offs, offs32);
 }
 
 void launch_scatter(int key_size, const SortDesc* d, const SegPlan* plan,
