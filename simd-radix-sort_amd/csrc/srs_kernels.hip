@@ -1289,13 +1289,19 @@ __global__ __launch_bounds__(NT, WPE) void local_kernel(const SortDesc* __restri
     const int lo = __ffsll((long long)var) - 1;
     const int hi = 63 - __clzll((long long)var);
     const bool exact = hi - lo + 1 <= kLocalTopBits;
-    // the sort word packs (key bits 0..hi, original index): needs hi+1+IDXB <= 64
-    if (!exact && hi + 1 + IDXB > 64) {
+    const int nbits = (hi - lo + 1) < kLocalTopBits ? (hi - lo + 1) : kLocalTopBits;
+    const int sh = hi - nbits + 1;
+    // The sort word packs (key bits 0..hi, original index) when that fits
+    // in 64 bits. Wide segments (hi+1+IDXB > 64: mid-size sorts of 64-bit
+    // keys) pack only the bits lo..sh-1 below the bucket digit (equal inside
+    // a bucket) and rank element-mapped with a masked loop; wider still goes
+    // to the stable kernel.
+    const bool wide = !exact && hi + 1 + IDXB > 64;
+    if (wide && sh - lo + IDXB > 64) {
       if (threadIdx.x == 0) fallback[atomicAdd(fallback_count, 1ull)] = g;
       return;
     }
-    const int nbits = (hi - lo + 1) < kLocalTopBits ? (hi - lo + 1) : kLocalTopBits;
-    const int sh = hi - nbits + 1;
+    const uint64_t below = (sh - lo >= 64) ? ~0ull : ((1ull << (sh - lo)) - 1);
     const uint32_t mask = (1u << nbits) - 1;
     const uint64_t keep = (hi == 63) ? ~0ull : ((1ull << (hi + 1)) - 1);
     if (exact) {
@@ -1399,7 +1405,8 @@ __global__ __launch_bounds__(NT, WPE) void local_kernel(const SortDesc* __restri
         const uint32_t d = (uint32_t)(uk >> sh) & mask;
         const uint32_t hs = (d & 1) << 4;
         const uint32_t p = (atomicAdd(&hist2[d >> 1], 1u << hs) >> hs) & 0xFFFFu;
-        sbuf[p] = (((uint64_t)uk & keep) << IDXB) | (uint64_t)(ebase + k * 64);
+        const uint64_t kw = wide ? (((uint64_t)uk >> lo) & below) : ((uint64_t)uk & keep);
+        sbuf[p] = (kw << IDXB) | (uint64_t)(ebase + k * 64);
       }
     }
     if (threadIdx.x < (uint32_t)kRankSortMax) sbuf[cnt + threadIdx.x] = ~0ull;  // sentinels
@@ -1409,6 +1416,9 @@ __global__ __launch_bounds__(NT, WPE) void local_kernel(const SortDesc* __restri
     // The word orders by (key, original index), so the result is stable.
     // Slots in two halves bound register use; a wave-uniform trip count
     // keeps several LDS reads in flight.
+    constexpr int NH = SRS_LOCAL_RANK_SPLIT;
+    constexpr int H = IT / NH;
+    if (!wide) {
     constexpr int NH = SRS_LOCAL_RANK_SPLIT;
     constexpr int H = IT / NH;
 #pragma unroll
@@ -1451,6 +1461,47 @@ __global__ __launch_bounds__(NT, WPE) void local_kernel(const SortDesc* __restri
       for (int i = 0; i < H; i++) {
         const int p = (half * H + i) * NT + (int)threadIdx.x;
         if (p < cnt) perm[bs[i] + r[i]] = (uint16_t)(x[i] & ((1u << IDXB) - 1));
+      }
+    }
+    } else {
+      // element-mapped: my own keys, their buckets recomputed; words past a
+      // bucket's end are not ordered against mine, so the loop is masked
+#pragma unroll
+      for (int half = 0; half < NH; half++) {
+        uint64_t x[H];
+        uint32_t bs[H], bl[H], r[H];
+        int wmax = 0;
+#pragma unroll
+        for (int i = 0; i < H; i++) {
+          const int k = half * H + i;
+          bl[i] = 0;
+          bs[i] = 0;
+          x[i] = 0;
+          r[i] = 0;
+          if (valid(k)) {
+            const U uk = ukey(k);
+            const uint32_t d = (uint32_t)(uk >> sh) & mask;
+            x[i] = ((((uint64_t)uk >> lo) & below) << IDXB) | (uint64_t)(ebase + k * 64);
+            bs[i] = bin_start[d];
+            bl[i] = bin_start[d + 1] - bs[i];
+            wmax = (int)bl[i] > wmax ? (int)bl[i] : wmax;
+          }
+        }
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) {
+          const int t2 = __shfl_xor(wmax, o, 64);
+          wmax = t2 > wmax ? t2 : wmax;
+        }
+        for (int j = 0; j < wmax; j++) {
+          uint64_t w[H];
+#pragma unroll
+          for (int i = 0; i < H; i++) w[i] = sbuf[bs[i] + (uint32_t)j];  // < CAP + kRankSortMax
+#pragma unroll
+          for (int i = 0; i < H; i++) r[i] += ((uint32_t)j < bl[i]) & (w[i] < x[i]);
+        }
+#pragma unroll
+        for (int i = 0; i < H; i++)
+          if (valid(half * H + i)) perm[bs[i] + r[i]] = (uint16_t)(ebase + (half * H + i) * 64);
       }
     }
     lds_barrier();

@@ -169,7 +169,10 @@ def test_sizes_u64_vs_oracle(n):
 
 
 def _fallback_keys(case, n, rng):
-    if case == "random64":  # full 64-bit range: too wide for packed words -> stable (wide words)
+    if case in ("random64", "mid64"):
+        # random64 (one local segment): the full 64-bit range is too wide even for the fast
+        # kernel's below-digit words -> stable kernel (key-only words). mid64: after one
+        # global level the segments' ranges fit the fast kernel's wide mode -> no fallback
         return rng.integers(0, 1 << 64, n, dtype=np.uint64)
     if case == "dups":      # big all-equal buckets: fast kernel -> stable kernel
         k = np.full(n, 0x1234_5678_9ABC, dtype=np.uint64)
@@ -187,6 +190,7 @@ def _fallback_keys(case, n, rng):
 
 
 @pytest.mark.parametrize("case,n", [("random64", 16), ("random64", 3000), ("random64", 8000),
+                                    ("mid64", 1 << 20), ("mid64", 100_003),
                                     ("dups", 3000), ("dups", 8000), ("wide", 3000),
                                     ("wide", 8000), ("groups", 300_000)])
 def test_local_fallback_paths(case, n):
@@ -207,6 +211,9 @@ def test_local_fallback_paths(case, n):
         srs_amd.set_kernel_timing(False)
     order = np.argsort(keys, kind="stable")
     assert bytes_equal(k, keys[order]) and bytes_equal(p, idx[order])
+    if case == "mid64":
+        assert stable_n == 0 and lsd_n == 0, "the fast kernel should have sorted every segment"
+        return
     assert stable_n > 0, "stable fallback not exercised"
     if case in ("wide", "groups"):
         assert lsd_n > 0, "LSD fallback not exercised"
