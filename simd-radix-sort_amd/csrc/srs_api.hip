@@ -350,6 +350,7 @@ int plan_balanced_level(Workspace* W, const Request& R, const SortDesc& d, bool*
 struct LevelState {
   int64_t nbig, n_local, n_local2, n_copy;
   int cur;
+  int64_t known_len = -1;  // the length of the single big segment, when the host knows it
 };
 
 // One global MSB level over every large segment in W->big[S.cur]:
@@ -388,12 +389,24 @@ int run_level(Workspace* W, int ks, const SortDesc* d_desc, LevelState& S, int f
                      (uint64_t*)W->scan_tmp.p, d_totals + 1, st);
     launch_plan_bases(plan, nbig, (int64_t*)W->tbase.p, (int64_t*)W->gbase.p, st);
   }
-  HIP_TRY(hipMemcpyAsync(W->h_totals, d_totals, 4 * sizeof(uint64_t),
-                         hipMemcpyDeviceToHost, st));
-  HIP_TRY(hipStreamSynchronize(st));
-  const int64_t ntiles = (int64_t)W->h_totals[0];
-  const int64_t ngroups = (int64_t)W->h_totals[1];
-  const double level_elems = (double)W->h_totals[3];
+  int64_t ntiles, ngroups;
+  uint64_t level_keys;
+  if (nbig == 1 && S.known_len >= 0) {
+    // the first level of a plain sort: the sizes follow from n (make_plan's
+    // formulas), so no read-back and no host wait
+    level_keys = (uint64_t)S.known_len;
+    ntiles = (S.known_len + kTile - 1) / kTile;
+    ngroups = (ntiles + kScanGroup - 1) / kScanGroup;
+  } else {
+    HIP_TRY(hipMemcpyAsync(W->h_totals, d_totals, 4 * sizeof(uint64_t),
+                           hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    ntiles = (int64_t)W->h_totals[0];
+    ngroups = (int64_t)W->h_totals[1];
+    level_keys = W->h_totals[3];
+  }
+  S.known_len = -1;
+  const double level_elems = (double)level_keys;
   note_elems("count", level_elems);
   note_elems("scatter", level_elems);
 
@@ -402,7 +415,7 @@ int run_level(Workspace* W, int ks, const SortDesc* d_desc, LevelState& S, int f
   SRS_TRY(ensure(W->hist, (size_t)ntiles * kMaxBins * 2));
   // u16 tile counts; u32 tile offsets when every segment of the level is
   // < 2^32 keys (all of them are when the level is), else u64
-  const bool offs32 = W->h_totals[3] < (1ull << 32);
+  const bool offs32 = level_keys < (1ull << 32);
   SRS_TRY(ensure(W->offs, (size_t)ntiles * kMaxBins * (offs32 ? 4 : 8)));
   SRS_TRY(ensure(W->gsum, (size_t)ngroups * kMaxBins * 4));
   SRS_TRY(ensure(W->gofs, (size_t)ngroups * kMaxBins * 8));
@@ -577,6 +590,7 @@ int run_sort(Workspace* W, const Request& R, hipStream_t st) {
     W->h_ctr->local_elems = to_local ? (uint64_t)n : 0;
   }
   LevelState S{n_big, n_local, n_local2, n_copy, 0};
+  if (R.nsegs == 0 && n_big == 1) S.known_len = n;
   int level = 0;
   if (balanced && S.nbig > 0) {
     ++level;
