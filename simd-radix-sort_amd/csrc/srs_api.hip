@@ -625,10 +625,13 @@ int run_sort(Workspace* W, const Request& R, hipStream_t st) {
     }
     {
       TimedScope ts2("local_stable", 0, st);
-      // one workgroup per segment that could have been handed over (the
-      // list length is only known on device; surplus workgroups exit at once)
-      if (n_local2 > 0) launch_local_stable(ksl, d_desc, fb, nfb, 1, fb2, nfb2, (int)n_local2, st);
-      if (n_local > 0) launch_local_stable(ksl, d_desc, fb1, nfb1, 0, fb2, nfb2, (int)n_local, st);
+      // grid-stride over the handed-over segments (the list length is only
+      // known on device): at most 2048 workgroups, so an empty list costs a
+      // few microseconds instead of one exiting workgroup per local segment
+      // (0.11 ms at C1)
+      auto grid = [](int64_t m) { return (int)std::min<int64_t>(m, 2048); };
+      if (n_local2 > 0) launch_local_stable(ksl, d_desc, fb, nfb, 1, fb2, nfb2, grid(n_local2), st);
+      if (n_local > 0) launch_local_stable(ksl, d_desc, fb1, nfb1, 0, fb2, nfb2, grid(n_local), st);
     }
     {
       TimedScope ts3("local_lsd", 0, st);
