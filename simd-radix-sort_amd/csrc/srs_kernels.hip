@@ -941,14 +941,9 @@ __global__ __launch_bounds__(kMaxBins) void tile_offs_kernel(
 // Column 0 holds the key in its low bytes (SoA: the key column; AoS: the
 // record's first <=8-byte slice). A tile's loads (column 0, the first payload
 // column, its row of bucket offsets) are issued together; stores are never
-// waited for (LDS-only barriers between columns).
-//
-// scatter_pipe_kernel is persistent: each workgroup walks a contiguous chunk
-// of tiles and issues tile t+1's loads BEFORE tile t's ranking and stores
-// (vmcnt counts loads and stores in issue order, so a load issued after a
-// store would wait for it). HBM then always has a tile's worth of loads in
-// flight per workgroup, and neighbouring tiles' runs into one bucket are
-// written by one workgroup (their partial lines meet in one L2).
+// waited for (LDS-only barriers between columns). One tile per workgroup,
+// two 16-wave workgroups per CU (<= 64 VGPRs); persistent variants that
+// prefetch the next tile measured slower.
 template <bool LUT>
 struct ScatterLds {
   uint64_t sval[kTile];
