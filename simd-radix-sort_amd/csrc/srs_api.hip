@@ -289,10 +289,10 @@ int plan_balanced_level(Workspace* W, const Request& R, const SortDesc& d, bool*
   constexpr int kChunk = 1024;
   const int64_t blocks = std::min<int64_t>(4096, n / kChunk);
   const int64_t stride = n / blocks;
-  SRS_TRY(ensure(W->shist, 65536 * sizeof(uint32_t)));
-  HIP_TRY(hipMemsetAsync(W->shist.p, 0, 65536 * sizeof(uint32_t), st));
+  // shist: the 64K-bin histogram, then the workgroups' partial rows
+  SRS_TRY(ensure(W->shist, 65536 * sizeof(uint32_t) + sample_partial_bytes()));
   launch_sample_hist16(R.in_cols[0], ks, n, stride, kChunk, blocks, d.mpos, d.mneg,
-                       (uint32_t*)W->shist.p, st);
+                       (uint32_t*)W->shist.p + 65536, (uint32_t*)W->shist.p, st);
   std::vector<uint32_t> h(65536);
   HIP_TRY(hipMemcpyAsync(h.data(), W->shist.p, h.size() * 4, hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));

@@ -1928,27 +1928,59 @@ __global__ __launch_bounds__(kLocalStableThreads) void local_lsd_kernel(
 }
 
 // ---------------------------------------------------------------------------
-// sampled 16-bit key histogram (balanced first level): block b
-// counts the transformed top 16 bits of keys [b*stride, b*stride + chunk)
-// ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void sample_hist16_kernel(
+// sampled 16-bit key histogram (balanced first level): chunk c
+// = keys [c*stride, c*stride + chunk). Each of kSampleWGs workgroups counts
+// its share of the chunks into LDS-private u16 bins (64K bins packed in
+// pairs: 128 KB of LDS; a workgroup counts < 65536 keys) and stores them as
+// one partial row; a second kernel sums the rows. Global atomics per key
+// (the previous form) took 0.16 ms for 4M keys.
+constexpr int kSampleWGs = 256;
+constexpr int kSampleThreads = 1024;
+
+__global__ __launch_bounds__(kSampleThreads) void sample_hist16_kernel(
     const char* __restrict__ keys, int key_bytes, int64_t n, int64_t stride, int chunk,
-    uint64_t mpos, uint64_t mneg, uint32_t* __restrict__ hist) {
+    int64_t nchunks, uint64_t mpos, uint64_t mneg, uint32_t* __restrict__ partial) {
+  __shared__ uint32_t h2[32768];
+  for (uint32_t i = threadIdx.x; i < 32768u; i += kSampleThreads) h2[i] = 0;
+  __syncthreads();
   const int kb = 8 * key_bytes;
-  const int64_t a = (int64_t)blockIdx.x * stride;
-  const int64_t e = min(n, a + chunk);
-  for (int64_t i = a + threadIdx.x; i < e; i += 256) {
-    const uint64_t bits = load_w(keys + i * key_bytes, key_bytes);
-    const uint64_t u = bits ^ (((bits >> (kb - 1)) & 1) ? mneg : mpos);
-    atomicAdd(&hist[(uint32_t)(u >> (kb - 16)) & 0xFFFF], 1u);
+  for (int64_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
+    const int64_t a = c * stride;
+    const int64_t e = min(n, a + chunk);
+    for (int64_t i = a + threadIdx.x; i < e; i += kSampleThreads) {
+      const uint64_t bits = load_w(keys + i * key_bytes, key_bytes);
+      const uint64_t u = bits ^ (((bits >> (kb - 1)) & 1) ? mneg : mpos);
+      const uint32_t d = (uint32_t)(u >> (kb - 16)) & 0xFFFFu;
+      atomicAdd(&h2[d >> 1], 1u << ((d & 1) << 4));
+    }
   }
+  __syncthreads();
+  uint32_t* row = partial + (int64_t)blockIdx.x * 32768;
+  for (uint32_t i = threadIdx.x; i < 32768u; i += kSampleThreads) row[i] = h2[i];
 }
 
+__global__ __launch_bounds__(256) void sample_reduce_kernel(const uint32_t* __restrict__ partial,
+                                                            int rows, uint32_t* __restrict__ hist) {
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;  // a pair of bins
+  uint32_t lo = 0, hi = 0;
+  for (int r = 0; r < rows; r++) {
+    const uint32_t v = partial[(int64_t)r * 32768 + i];
+    lo += v & 0xFFFFu;
+    hi += v >> 16;
+  }
+  hist[2 * i] = lo;
+  hist[2 * i + 1] = hi;
+}
+
+int64_t sample_partial_bytes() { return (int64_t)kSampleWGs * 32768 * 4; }
+
 void launch_sample_hist16(const void* keys, int key_bytes, int64_t n, int64_t stride, int chunk,
-                          int64_t blocks, uint64_t mpos, uint64_t mneg, uint32_t* hist,
-                          hipStream_t st) {
-  sample_hist16_kernel<<<(unsigned)blocks, 256, 0, st>>>((const char*)keys, key_bytes, n, stride,
-                                                         chunk, mpos, mneg, hist);
+                          int64_t blocks, uint64_t mpos, uint64_t mneg, uint32_t* partial,
+                          uint32_t* hist, hipStream_t st) {
+  const int wgs = (int)std::min<int64_t>(kSampleWGs, std::max<int64_t>(1, blocks));
+  sample_hist16_kernel<<<(unsigned)wgs, kSampleThreads, 0, st>>>(
+      (const char*)keys, key_bytes, n, stride, chunk, blocks, mpos, mneg, partial);
+  sample_reduce_kernel<<<32768 / 256, 256, 0, st>>>(partial, wgs, hist);
 }
 
 // ---------------------------------------------------------------------------
