@@ -337,7 +337,7 @@ int plan_balanced_level(Workspace* W, const Request& R, const SortDesc& d, bool*
   }
   if ((int)t2.size() > kLdsLutEntries) return fail(SRS_ERR_INTERNAL, "digit table too large");
   *lut_entries = (int)t2.size();
-  SRS_TRY(ensure(W->lut, t2.size() * sizeof(uint16_t)));
+  SRS_TRY(ensure(W->lut, align_up(t2.size() * sizeof(uint16_t), 16)));  // staged in 16-byte loads
   SRS_TRY(ensure(W->lut_rbits, kGroups * sizeof(int32_t)));
   HIP_TRY(hipMemcpyAsync(W->lut.p, t2.data(), t2.size() * 2, hipMemcpyHostToDevice, st));
   HIP_TRY(hipMemcpyAsync(W->lut_rbits.p, rbits.data(), rbits.size() * 4, hipMemcpyHostToDevice,

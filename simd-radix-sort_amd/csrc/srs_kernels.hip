@@ -601,14 +601,45 @@ __device__ __forceinline__ DigitLut stage_lut(const SortDesc* desc, uint16_t* sl
   if (!LUT) return L;
   L.shift = desc->lut_shift;
   L.mode = desc->lut_mode;
+  // 16-byte range-checked buffer loads, all in flight before any LDS store
+  // (a loop of 2-byte loads waited for each one: ~16-48 round trips per
+  // workgroup, and every LUT-level workgroup stages the table)
   if (L.mode == 1) {
-    const int n = desc->lut_entries;  // 4096 + 16 per split bin (<= kLdsLutEntries)
-    const uint16_t* src = (const uint16_t*)desc->digit_lut;
-    for (int i = threadIdx.x; i < n; i += NT) slut[i] = gld<uint16_t>(src + i);
+    const int n8 = (desc->lut_entries + 7) >> 3;  // 4096 + 16 per split bin (<= kLdsLutEntries)
+    constexpr int K = (kLdsLutEntries / 8 + NT - 1) / NT;
+    const __amdgpu_buffer_rsrc_t r = strip_rsrc((const char*)desc->digit_lut, (uint32_t)n8 * 16u);
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    u32x4 v[K];
+#pragma unroll
+    for (int k = 0; k < K; k++)
+      v[k] = __builtin_amdgcn_raw_buffer_load_b128(r, (threadIdx.x + (uint32_t)k * NT) * 16u, 0, 0);
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+      const int i = threadIdx.x + k * NT;
+      if (i < n8) ((u32x4*)slut)[i] = v[k];
+    }
+    L.s = slut;
+  } else if (desc->lut_bits < 2) {
+    for (int i = threadIdx.x; i < (1 << desc->lut_bits); i += NT)
+      slut[i] = (uint16_t)gld<int32_t>(desc->digit_lut + i);
     L.s = slut;
   } else if (desc->lut_bits <= kLdsLutBits) {
-    const int n = 1 << desc->lut_bits;
-    for (int i = threadIdx.x; i < n; i += NT) slut[i] = (uint16_t)gld<int32_t>(desc->digit_lut + i);
+    const int n4 = (1 << desc->lut_bits) >> 2;
+    constexpr int K = ((1 << kLdsLutBits) / 4 + NT - 1) / NT;
+    const __amdgpu_buffer_rsrc_t r = strip_rsrc((const char*)desc->digit_lut, (uint32_t)n4 * 16u);
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    u32x4 v[K];
+#pragma unroll
+    for (int k = 0; k < K; k++)
+      v[k] = __builtin_amdgcn_raw_buffer_load_b128(r, (threadIdx.x + (uint32_t)k * NT) * 16u, 0, 0);
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+      const int i = threadIdx.x + k * NT;
+      if (i < n4) {
+        ((uint32_t*)slut)[2 * i] = (v[k][0] & 0xFFFFu) | (v[k][1] << 16);
+        ((uint32_t*)slut)[2 * i + 1] = (v[k][2] & 0xFFFFu) | (v[k][3] << 16);
+      }
+    }
     L.s = slut;
   } else {
     L.g = desc->digit_lut;
@@ -636,7 +667,7 @@ __global__ __launch_bounds__(kCountThreads) void count_kernel(
   xf.init(*desc);
   const char* kp = desc->key.base[P.buf];
   const uint32_t ks = desc->key.stride;
-  __shared__ uint16_t slut[LUT ? kLdsLutEntries : 1];
+  __shared__ alignas(16) uint16_t slut[LUT ? kLdsLutEntries : 8];
   const DigitLut lut = stage_lut<LUT, kCountThreads>(desc, slut);
 
   for (uint32_t i = threadIdx.x; i < nb; i += kCountThreads) h[i] = 0;
@@ -1121,7 +1152,7 @@ __global__ __launch_bounds__(kScatterThreads, SRS_SCATTER_WAVES_PER_EU) void sca
     const int32_t* __restrict__ tile_seg, const uint64_t* __restrict__ offs,
     const uint32_t* __restrict__ offs32) {
   __shared__ ScatterLds<LUT> L;
-  __shared__ uint16_t slut[LUT ? kLdsLutEntries : 1];
+  __shared__ alignas(16) uint16_t slut[LUT ? kLdsLutEntries : 8];
   const int64_t t = xcd_remap(blockIdx.x, gridDim.x);
   const int ncols = desc->ncols;
   uint64_t v0[kScatterItems], v1[kScatterItems];
