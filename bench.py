@@ -223,6 +223,19 @@ def main():
     t1 = time.perf_counter()
     srs_amd.set_kernel_timing(False)
     elapsed = t1 - t0
+    # The timed steps carry HIP event markers around each launch (async
+    # stream packets, no host waits; the roofline's launch durations come
+    # from them). The same steps without the markers, for comparison:
+    torch.cuda.synchronize()
+    if shard:
+        dist.barrier()
+    t2 = time.perf_counter()
+    for _ in range(min(args.steps, 3)):
+        step()
+    torch.cuda.synchronize()
+    if shard:
+        dist.barrier()
+    ms_no_events = (time.perf_counter() - t2) / min(args.steps, 3) * 1e3
     if shard:
         tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -283,6 +296,7 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 3),
+            "ms_per_step_without_event_markers": round(ms_no_events, 3),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,

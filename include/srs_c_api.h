@@ -191,6 +191,12 @@ int srs_kernel_stats(const char* name, int64_t* launches, double* total_ms,
  * local (16..31) kernels; NULL disables. No effect in the product build. */
 int srs_debug_set_stamp_buffer(void* device_acc);
 
+/* Segments the local-level fallback kernels took in the last sort on the
+ * current device: counts[0] = handed to the stable kernel, counts[1] = handed
+ * on to the LSD kernel. Synchronizes the device. Tests use it to prove that
+ * an input exercised a given path. */
+int srs_debug_last_fallbacks(int64_t* counts);
+
 /* Release cached device workspaces (for leak checks / shutdown). */
 int srs_release_workspace(void);
 

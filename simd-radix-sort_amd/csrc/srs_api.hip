@@ -196,6 +196,12 @@ struct Workspace {
   DevBuf shist, lut, lut_rbits;  // balanced first level (sampled histogram, digit table)
   ListCounters* h_ctr = nullptr;
   uint64_t* h_totals = nullptr;
+  // Stream order of the workspace: the last call's kernels may still be
+  // queued on its stream when the call returns. `idle` is recorded on that
+  // stream at the end of every call; the next call's stream waits for it
+  // before its first workspace write (WsUse).
+  hipEvent_t idle = nullptr;
+  bool idle_pending = false;
 };
 
 std::mutex g_wmu;
@@ -218,6 +224,24 @@ int get_ws(Workspace** out) {
 }
 
 size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+// Holds the workspace for one call on stream `st` (under g_wmu): waits on the
+// device for the previous call's work on the workspace (any stream), and
+// marks the end of this call's work when it goes out of scope, also on error.
+struct WsUse {
+  Workspace* W = nullptr;
+  hipStream_t st = nullptr;
+  int begin(Workspace* w, hipStream_t s) {
+    W = w;
+    st = s;
+    if (!W->idle) HIP_TRY(hipEventCreateWithFlags(&W->idle, hipEventDisableTiming));
+    if (W->idle_pending) HIP_TRY(hipStreamWaitEvent(st, W->idle, 0));
+    return SRS_OK;
+  }
+  ~WsUse() {
+    if (W && W->idle) W->idle_pending = hipEventRecord(W->idle, st) == hipSuccess;
+  }
+};
 
 
 // ---------------------------------------------------------------------------
@@ -286,13 +310,13 @@ int plan_balanced_level(Workspace* W, const Request& R, const SortDesc& d, bool*
   const int ks = key_size_of(R.kind);
   const int64_t n = R.num;
   if (R.nsegs > 0 || R.aos || n < kBalancedMinN || ks < 4) return SRS_OK;
-  constexpr int kChunk = 1024;
-  const int64_t blocks = std::min<int64_t>(4096, n / kChunk);
+  const int64_t blocks = std::min<int64_t>(kSampleMaxChunks, n / kSampleChunk);
   const int64_t stride = n / blocks;
   // shist: the 64K-bin histogram, then the workgroups' partial rows
   SRS_TRY(ensure(W->shist, 65536 * sizeof(uint32_t) + sample_partial_bytes()));
-  launch_sample_hist16(R.in_cols[0], ks, n, stride, kChunk, blocks, d.mpos, d.mneg,
-                       (uint32_t*)W->shist.p + 65536, (uint32_t*)W->shist.p, st);
+  if (!launch_sample_hist16(R.in_cols[0], ks, n, stride, kSampleChunk, blocks, d.mpos, d.mneg,
+                            (uint32_t*)W->shist.p + 65536, (uint32_t*)W->shist.p, st))
+    return fail(SRS_ERR_INTERNAL, "sample histogram: too many keys per workgroup");
   std::vector<uint32_t> h(65536);
   HIP_TRY(hipMemcpyAsync(h.data(), W->shist.p, h.size() * 4, hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
@@ -638,17 +662,15 @@ int run_sort(Workspace* W, const Request& R, hipStream_t st) {
       const int fgrid = (int)std::min<int64_t>(512, n_local + n_local2);
       launch_local_lsd(ksl, d_desc, fb2, nfb2, fgrid, st);
     }
-    if (timing_enabled() || trace_levels()) {
-      // diagnostics: how many segments took each fallback
+    if (trace_levels()) {
+      // diagnostics: how many segments took each fallback (a host wait; kept
+      // out of the timing mode, which only adds event markers)
       ListCounters c;
       HIP_TRY(hipMemcpyAsync(&c, d_ctr, sizeof(c), hipMemcpyDeviceToHost, st));
       HIP_TRY(hipStreamSynchronize(st));
-      note_elems("local_stable", (double)(c.n_fallback + c.n_fallback1));
-      note_elems("local_lsd", (double)c.n_fallback2);
-      if (trace_levels())
-        fprintf(stderr, "[srs] local: %lld + %lld segs (%llu keys); stable fallback %llu + %llu, "
-                "lsd fallback %llu\n", (long long)n_local, (long long)n_local2,
-                c.local_elems, c.n_fallback1, c.n_fallback, c.n_fallback2);
+      fprintf(stderr, "[srs] local: %lld + %lld segs (%llu keys); stable fallback %llu + %llu, "
+              "lsd fallback %llu\n", (long long)n_local, (long long)n_local2,
+              c.local_elems, c.n_fallback1, c.n_fallback, c.n_fallback2);
     }
   }
   if (n_copy > 0) {
@@ -753,6 +775,8 @@ int sort_device(Request& R, hipStream_t st) {
   std::lock_guard<std::mutex> lk(g_wmu);
   Workspace* W = nullptr;
   SRS_TRY(get_ws(&W));
+  WsUse use;
+  SRS_TRY(use.begin(W, st));
   return run_sort(W, R, st);
 }
 
@@ -772,8 +796,10 @@ int sort_host(Request& R) {
     const size_t w = R.aos ? R.elem_size : R.widths[c];
     total += align_up((size_t)R.num * w, 256);
   }
-  SRS_TRY(ensure(W->stage, total));
   hipStream_t st = nullptr;
+  WsUse use;
+  SRS_TRY(use.begin(W, st));
+  SRS_TRY(ensure(W->stage, total));
   Request D = R;
   for (int c = 0; c < R.ncols; c++) {
     const size_t w = R.aos ? R.elem_size : R.widths[c];
@@ -900,6 +926,8 @@ int srs_sort_segments_device(int64_t num, int key_kind, int up, void* keys,
   std::lock_guard<std::mutex> lk(g_wmu);
   Workspace* W = nullptr;
   SRS_TRY(get_ws(&W));
+  WsUse use;
+  SRS_TRY(use.begin(W, (hipStream_t)stream));
   return run_sort(W, R, (hipStream_t)stream);
 }
 
@@ -992,6 +1020,8 @@ int srs_partition_device(int64_t num, int key_kind, int up, const void* keys,
   std::lock_guard<std::mutex> lk(g_wmu);
   Workspace* W = nullptr;
   SRS_TRY(get_ws(&W));
+  WsUse use;
+  SRS_TRY(use.begin(W, (hipStream_t)stream));
   return run_partition(W, R, bits, part_of_bucket, num_parts, part_counts, (hipStream_t)stream);
 }
 
@@ -1029,10 +1059,29 @@ int srs_debug_set_stamp_buffer(void* device_acc) {
   return SRS_OK;
 }
 
+int srs_debug_last_fallbacks(int64_t* counts) {
+  if (!counts) return fail(SRS_ERR_INVALID_ARG, "counts is NULL");
+  std::lock_guard<std::mutex> lk(g_wmu);
+  Workspace* W = nullptr;
+  SRS_TRY(get_ws(&W));
+  counts[0] = counts[1] = 0;
+  if (!W->ctr.p) return SRS_OK;
+  HIP_TRY(hipDeviceSynchronize());
+  ListCounters c;
+  HIP_TRY(hipMemcpy(&c, W->ctr.p, sizeof c, hipMemcpyDeviceToHost));
+  counts[0] = (int64_t)(c.n_fallback + c.n_fallback1);
+  counts[1] = (int64_t)c.n_fallback2;
+  return SRS_OK;
+}
+
 int srs_release_workspace(void) {
   std::lock_guard<std::mutex> lk(g_wmu);
   for (auto& kv : g_ws) {
     Workspace* w = kv.second;
+    if (w->idle) {  // the last call's kernels may still read the buffers
+      (void)hipEventSynchronize(w->idle);
+      (void)hipEventDestroy(w->idle);
+    }
     DevBuf* bufs[] = {&w->tmp, &w->stage, &w->desc, &w->big[0], &w->big[1], &w->local, &w->local2, &w->fallback, &w->fallback2, &w->shist, &w->lut, &w->lut_rbits,
                       &w->copy, &w->plan, &w->tcount, &w->gcount, &w->tbase, &w->gbase,
                       &w->var, &w->sbase, &w->tile_seg, &w->group_seg, &w->hist, &w->offs,

@@ -116,6 +116,13 @@ constexpr int kScanGroup = 256;                 // tiles per column-scan group
 constexpr int kHistMaxBits = 12;                // srs_key_histogram_device
 constexpr int kLdsLutBits = 12;                 // flat digit tables up to 4096 entries live in LDS
 constexpr int kLdsLutEntries = 4096 + 16 * 512; // two-level table worst case (24 KB of u16)
+// sampled 16-bit skew histogram (balanced first level): workgroups, and the
+// sample's shape; a workgroup's packed u16 LDS bins hold < 65536 keys
+constexpr int kSampleWGs = 256;
+constexpr int kSampleChunk = 1024;      // contiguous keys per sampled chunk
+constexpr int kSampleMaxChunks = 4096;
+static_assert((kSampleMaxChunks + kSampleWGs - 1) / kSampleWGs * kSampleChunk < 65536,
+              "sample histogram: u16 bins per workgroup");
 
 // local sort classes: fast kernel (atomic bucket pass + rank) in two sizes,
 // then the stable kernel and the LSD kernel as fallbacks (same capacity as

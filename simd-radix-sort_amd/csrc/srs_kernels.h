@@ -46,7 +46,7 @@ void launch_local_stable(int key_size, const SortDesc* d, const Seg* segs,
 void launch_local_lsd(int key_size, const SortDesc* d, const Seg* segs,
                       const unsigned long long* nsegs, int grid, hipStream_t st);
 int64_t sample_partial_bytes();
-void launch_sample_hist16(const void* keys, int key_bytes, int64_t n, int64_t stride, int chunk,
+bool launch_sample_hist16(const void* keys, int key_bytes, int64_t n, int64_t stride, int chunk,
                           int64_t blocks, uint64_t mpos, uint64_t mneg, uint32_t* partial,
                           uint32_t* hist, hipStream_t st);
 void launch_fill(int64_t n, int kind, uint64_t seed, uint64_t first, void* keys,

@@ -1965,7 +1965,6 @@ __global__ __launch_bounds__(kLocalStableThreads) void local_lsd_kernel(
 // pairs: 128 KB of LDS; a workgroup counts < 65536 keys) and stores them as
 // one partial row; a second kernel sums the rows. Global atomics per key
 // (the previous form) took 0.16 ms for 4M keys.
-constexpr int kSampleWGs = 256;
 constexpr int kSampleThreads = 1024;
 
 __global__ __launch_bounds__(kSampleThreads) void sample_hist16_kernel(
@@ -2005,13 +2004,16 @@ __global__ __launch_bounds__(256) void sample_reduce_kernel(const uint32_t* __re
 
 int64_t sample_partial_bytes() { return (int64_t)kSampleWGs * 32768 * 4; }
 
-void launch_sample_hist16(const void* keys, int key_bytes, int64_t n, int64_t stride, int chunk,
+bool launch_sample_hist16(const void* keys, int key_bytes, int64_t n, int64_t stride, int chunk,
                           int64_t blocks, uint64_t mpos, uint64_t mneg, uint32_t* partial,
                           uint32_t* hist, hipStream_t st) {
   const int wgs = (int)std::min<int64_t>(kSampleWGs, std::max<int64_t>(1, blocks));
+  // the packed u16 bins of one workgroup must not carry into their neighbour
+  if ((blocks + wgs - 1) / wgs * (int64_t)chunk >= 65536) return false;
   sample_hist16_kernel<<<(unsigned)wgs, kSampleThreads, 0, st>>>(
       (const char*)keys, key_bytes, n, stride, chunk, blocks, mpos, mneg, partial);
   sample_reduce_kernel<<<32768 / 256, 256, 0, st>>>(partial, wgs, hist);
+  return true;
 }
 
 // ---------------------------------------------------------------------------

@@ -69,6 +69,7 @@ def lib() -> ctypes.CDLL:
                                            vp]
     L.srs_partition_device.argtypes = [i64, ctypes.c_int, ctypes.c_int, vp, i32, vp, vp,
                                        ctypes.c_int, vp, i32, vp, vp, vp, vp]
+    L.srs_debug_last_fallbacks.argtypes = [ctypes.POINTER(i64)]
     L.srs_last_error.restype = ctypes.c_char_p
     L.srs_version.restype = ctypes.c_char_p
     L.srs_set_kernel_timing.argtypes = [ctypes.c_int]
@@ -161,20 +162,35 @@ def _torch_kind(t) -> int:
     return _TORCH_KIND[t.dtype]
 
 
-def _stream_ptr(stream=None) -> int:
+def _stream_ptr(stream=None, device=None) -> int:
     import torch
-    s = stream if stream is not None else torch.cuda.current_stream()
+    s = stream if stream is not None else torch.cuda.current_stream(device)
     return s.cuda_stream
+
+
+def _on_device(t):
+    """Context that makes t's GPU the current HIP device: the library picks
+    its workspace (and torch its current stream) from the current device."""
+    import torch
+    return torch.cuda.device(t.device)
+
+
+def _check_columns(keys, cols, what="tensors"):
+    """Every column is a 1-D contiguous tensor on keys' GPU with keys' length."""
+    for t in cols:
+        if not (t.is_cuda and t.is_contiguous() and t.dim() == 1 and t.numel() == keys.numel()):
+            raise ValueError(f"{what} must be 1-D contiguous device tensors of equal length")
+        if t.device != keys.device:
+            raise ValueError(f"{what} must all be on {keys.device} (got {t.device})")
 
 
 def sort_device(keys, *payloads, up: bool = True, cmp_sort_threshold: int = 16,
                 key_kind: int | None = None, out=None, stream=None) -> None:
     """Sort device tensors. In place unless `out` = (keys_out, *payloads_out).
     `key_kind` overrides the kind derived from keys.dtype (e.g. torch.int64
-    storage holding uint64 keys)."""
-    for t in (keys,) + payloads:
-        if not (t.is_cuda and t.is_contiguous() and t.dim() == 1 and t.numel() == keys.numel()):
-            raise ValueError("tensors must be 1-D contiguous device tensors of equal length")
+    storage holding uint64 keys). Runs on keys' GPU, on `stream` or that
+    GPU's current stream."""
+    _check_columns(keys, (keys,) + payloads)
     kind = _torch_kind(keys) if key_kind is None else int(key_kind)
     np_ = len(payloads)
     pays = _ptr_array([p.data_ptr() for p in payloads])
@@ -182,13 +198,18 @@ def sort_device(keys, *payloads, up: bool = True, cmp_sort_threshold: int = 16,
     if out is not None:
         if len(out) != 1 + np_:
             raise ValueError("out must hold keys_out followed by every payload_out")
+        _check_columns(keys, tuple(out), "out tensors")
+        for o, i in zip(out, (keys,) + payloads):
+            if o.element_size() != i.element_size():
+                raise ValueError("every out tensor must have its input's element size")
         kout = out[0].data_ptr()
         pout = _ptr_array([o.data_ptr() for o in out[1:]])
     else:
         kout, pout = None, None
-    _check(lib().srs_sort_soa_device(keys.numel(), kind, int(bool(up)), int(cmp_sort_threshold),
-                                     keys.data_ptr(), np_, pays, sizes, kout, pout,
-                                     _stream_ptr(stream)))
+    with _on_device(keys):
+        _check(lib().srs_sort_soa_device(keys.numel(), kind, int(bool(up)),
+                                         int(cmp_sort_threshold), keys.data_ptr(), np_, pays,
+                                         sizes, kout, pout, _stream_ptr(stream, keys.device)))
 
 
 def sort_segments_device(keys, *payloads, bounds, up: bool = True, key_kind: int | None = None,
@@ -197,27 +218,34 @@ def sort_segments_device(keys, *payloads, bounds, up: bool = True, key_kind: int
     independently, in place (srs_sort_segments_device). `bounds`: host
     sequence of non-decreasing offsets; `known_top_bits`: top transformed
     key bits every segment's keys are known to share."""
-    for t in (keys,) + payloads:
-        if not (t.is_cuda and t.is_contiguous() and t.dim() == 1 and t.numel() == keys.numel()):
-            raise ValueError("tensors must be 1-D contiguous device tensors of equal length")
+    _check_columns(keys, (keys,) + payloads)
     kind = _torch_kind(keys) if key_kind is None else int(key_kind)
     b = (ctypes.c_int64 * len(bounds))(*[int(x) for x in bounds])
-    _check(lib().srs_sort_segments_device(
-        keys.numel(), kind, int(bool(up)), keys.data_ptr(), len(payloads),
-        _ptr_array([p.data_ptr() for p in payloads]), _size_array([p.element_size() for p in payloads]),
-        max(0, len(bounds) - 1), b, int(known_top_bits), _stream_ptr(stream)))
+    with _on_device(keys):
+        _check(lib().srs_sort_segments_device(
+            keys.numel(), kind, int(bool(up)), keys.data_ptr(), len(payloads),
+            _ptr_array([p.data_ptr() for p in payloads]),
+            _size_array([p.element_size() for p in payloads]),
+            max(0, len(bounds) - 1), b, int(known_top_bits), _stream_ptr(stream, keys.device)))
 
 
 def sort_combined_device(elements, key_kind: int, up: bool = True,
                          cmp_sort_threshold: int = 16, out=None, stream=None) -> None:
     """DataElement array on the device: `elements` is a contiguous (n, elem_size)
     uint8 tensor (or any contiguous tensor whose first dim is the record)."""
+    if not (elements.is_cuda and elements.is_contiguous()):
+        raise ValueError("elements must be a contiguous device tensor")
     n = elements.shape[0]
     esz = elements.numel() * elements.element_size() // max(1, n)
-    _check(lib().srs_sort_aos_device(n, int(key_kind), int(bool(up)), int(cmp_sort_threshold),
-                                     elements.data_ptr(), esz,
-                                     None if out is None else out.data_ptr(),
-                                     _stream_ptr(stream)))
+    if out is not None:
+        if not (out.is_cuda and out.is_contiguous() and out.device == elements.device and
+                out.numel() * out.element_size() == elements.numel() * elements.element_size()):
+            raise ValueError("out must be a contiguous tensor of the same bytes on the same GPU")
+    with _on_device(elements):
+        _check(lib().srs_sort_aos_device(n, int(key_kind), int(bool(up)), int(cmp_sort_threshold),
+                                         elements.data_ptr(), esz,
+                                         None if out is None else out.data_ptr(),
+                                         _stream_ptr(stream, elements.device)))
 
 
 def fill_synthetic_device(keys, *payloads, seed: int = 42 << 32, first_index: int = 0,
@@ -225,11 +253,13 @@ def fill_synthetic_device(keys, *payloads, seed: int = 42 << 32, first_index: in
     """keys[i] = splitmix64(seed + first_index + i) (see srs_c_api.h);
     payloads are functions of the key."""
     kind = _torch_kind(keys) if key_kind is None else int(key_kind)
-    _check(lib().srs_fill_synthetic_device(keys.numel(), kind, seed, first_index,
-                                           keys.data_ptr(), len(payloads),
-                                           _ptr_array([p.data_ptr() for p in payloads]),
-                                           _size_array([p.element_size() for p in payloads]),
-                                           _stream_ptr(stream)))
+    _check_columns(keys, (keys,) + payloads)
+    with _on_device(keys):
+        _check(lib().srs_fill_synthetic_device(keys.numel(), kind, seed, first_index,
+                                               keys.data_ptr(), len(payloads),
+                                               _ptr_array([p.data_ptr() for p in payloads]),
+                                               _size_array([p.element_size() for p in payloads]),
+                                               _stream_ptr(stream, keys.device)))
 
 
 # --------------------------------------------------------------------------
@@ -242,8 +272,13 @@ def key_histogram_device(keys, hist, bits: int, up: bool = True, key_kind: int |
     kind = _torch_kind(keys) if key_kind is None else int(key_kind)
     if hist.numel() != (1 << bits) or hist.element_size() != 8 or not hist.is_cuda:
         raise ValueError("hist must be a device tensor of 2^bits 64-bit counters")
-    _check(lib().srs_key_histogram_device(keys.numel(), kind, int(bool(up)), keys.data_ptr(),
-                                          int(bits), hist.data_ptr(), _stream_ptr(stream)))
+    _check_columns(keys, (keys,))
+    if hist.device != keys.device or not hist.is_contiguous():
+        raise ValueError("hist must be contiguous and on the keys' GPU")
+    with _on_device(keys):
+        _check(lib().srs_key_histogram_device(keys.numel(), kind, int(bool(up)), keys.data_ptr(),
+                                              int(bits), hist.data_ptr(),
+                                              _stream_ptr(stream, keys.device)))
 
 
 def partition_device(keys, payloads, bits: int, part_of_bucket, num_parts: int, out,
@@ -254,13 +289,26 @@ def partition_device(keys, payloads, bits: int, part_of_bucket, num_parts: int, 
     kind = _torch_kind(keys) if key_kind is None else int(key_kind)
     if part_of_bucket.dtype.itemsize != 4 or part_of_bucket.numel() != (1 << bits):
         raise ValueError("part_of_bucket must hold 2^bits int32 entries")
-    counts = (ctypes.c_int64 * num_parts)()
     pays = list(payloads)
-    _check(lib().srs_partition_device(
-        keys.numel(), kind, int(bool(up)), keys.data_ptr(), len(pays),
-        _ptr_array([p.data_ptr() for p in pays]), _size_array([p.element_size() for p in pays]),
-        int(bits), part_of_bucket.data_ptr(), int(num_parts), out[0].data_ptr(),
-        _ptr_array([o.data_ptr() for o in out[1:]]), counts, _stream_ptr(stream)))
+    _check_columns(keys, [keys] + pays)
+    if not (part_of_bucket.is_cuda and part_of_bucket.device == keys.device and
+            part_of_bucket.is_contiguous()):
+        raise ValueError("part_of_bucket must be a contiguous tensor on the keys' GPU")
+    if len(out) != 1 + len(pays):
+        raise ValueError("out must hold keys_out followed by every payload_out")
+    for o, i in zip(out, [keys] + pays):
+        if not (o.is_cuda and o.device == keys.device and o.is_contiguous() and o.dim() == 1 and
+                o.numel() >= keys.numel() and o.element_size() == i.element_size()):
+            raise ValueError("out tensors must be contiguous, on the keys' GPU, at least as long "
+                             "as the input and of its element size")
+    counts = (ctypes.c_int64 * num_parts)()
+    with _on_device(keys):
+        _check(lib().srs_partition_device(
+            keys.numel(), kind, int(bool(up)), keys.data_ptr(), len(pays),
+            _ptr_array([p.data_ptr() for p in pays]), _size_array([p.element_size() for p in pays]),
+            int(bits), part_of_bucket.data_ptr(), int(num_parts), out[0].data_ptr(),
+            _ptr_array([o.data_ptr() for o in out[1:]]), counts,
+            _stream_ptr(stream, keys.device)))
     return [int(c) for c in counts]
 
 
@@ -283,6 +331,14 @@ def kernel_stats(name: str):
     _check(lib().srs_kernel_stats(name.encode(), ctypes.byref(n), ctypes.byref(ms),
                                   ctypes.byref(el)))
     return n.value, ms.value, el.value
+
+
+def last_fallbacks():
+    """(stable, lsd): local segments the last sort on the current device
+    handed to the stable / LSD fallback kernels (synchronizes the device)."""
+    c = (ctypes.c_int64 * 2)()
+    _check(lib().srs_debug_last_fallbacks(c))
+    return int(c[0]), int(c[1])
 
 
 def release_workspace() -> None:

@@ -105,7 +105,7 @@ class ShardSorter:
         self.ops = ops
         self.key_bits = 8 * torch.empty(0, dtype=key_dtype).element_size()
         self.bits = min(bits, self.key_bits)
-        self.groups = min(groups, 512, 1 << bits)
+        self.groups = min(groups, 512, 1 << self.bits)
         self.rounds = max(1, rounds)
         self.group = group
         self.world = dist.get_world_size(group)

@@ -64,7 +64,7 @@ class NumpyShardOps:
         pass
 
 
-def _worker(rank, world, port, kind, n_per, dist_kind, q):
+def _worker(rank, world, port, kind, n_per, dist_kind, q, bits=8):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "simd-radix-sort_amd",
@@ -72,7 +72,7 @@ def _worker(rank, world, port, kind, n_per, dist_kind, q):
     from srs_amd.dist import ShardSorter
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        _run(rank, world, kind, n_per, dist_kind, q)
+        _run(rank, world, kind, n_per, dist_kind, q, bits)
     except Exception as e:  # report instead of hanging the parent
         q.put(("error", repr(e)))
         raise
@@ -80,7 +80,7 @@ def _worker(rank, world, port, kind, n_per, dist_kind, q):
         dist.destroy_process_group()
 
 
-def _run(rank, world, kind, n_per, dist_kind, q):
+def _run(rank, world, kind, n_per, dist_kind, q, bits=8):
     from srs_amd.dist import ShardSorter
     if True:
         rng = np.random.default_rng(100 + rank)
@@ -95,8 +95,10 @@ def _run(rank, world, kind, n_per, dist_kind, q):
             k = np.full(n, 7, dtype=ut)
         keys = torch.from_numpy(k.copy())
         pay = torch.from_numpy(np.arange(n, dtype=np.int64) + rank * 10**9)
-        sorter = ShardSorter(NumpyShardOps(kind), n, [torch.int64], keys.dtype, "cpu", bits=8,
+        sorter = ShardSorter(NumpyShardOps(kind), n, [torch.int64], keys.dtype, "cpu", bits=bits,
                              chunk_bytes=1024)  # many exchange rounds
+        # never more groups than histogram bins of the (clamped) key width
+        assert sorter.groups <= 1 << sorter.bits
         ok, (op,) = sorter.sort(keys, [pay])
         mine = ok.numpy().copy()
         u = transformed_keys(kind, True, mine)
@@ -126,13 +128,11 @@ def _run(rank, world, kind, n_per, dist_kind, q):
             q.put((sorted_ok, True, True, None))
 
 
-@pytest.mark.parametrize("world", [2, 3, 4])
-@pytest.mark.parametrize("dist_kind", ["uniform", "skewed", "equal"])
-def test_shard_sort_gloo(world, dist_kind):
+def _run_world(world, kind, dist_kind, bits=8):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, 6, 3000, dist_kind, q))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, kind, 3000, dist_kind, q, bits))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -147,6 +147,18 @@ def test_shard_sort_gloo(world, dist_kind):
     nonempty = [x for x in b if x[0] >= 0]
     for a, c in zip(nonempty, nonempty[1:]):
         assert a[1] <= c[0]  # last key of rank r <= first key of rank r+1
+
+
+@pytest.mark.parametrize("world", [2, 3, 4])
+@pytest.mark.parametrize("dist_kind", ["uniform", "skewed", "equal"])
+def test_shard_sort_gloo(world, dist_kind):
+    _run_world(world, 6, dist_kind)
+
+
+@pytest.mark.parametrize("kind", [0, 3])  # u8, i16: keys narrower than the default 12 bits
+@pytest.mark.parametrize("dist_kind", ["uniform", "skewed"])
+def test_shard_sort_gloo_narrow_keys(kind, dist_kind):
+    _run_world(2, kind, dist_kind, bits=12)
 
 
 def test_balanced_split_is_monotone_and_balanced():

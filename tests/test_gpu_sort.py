@@ -195,20 +195,14 @@ def _fallback_keys(case, n, rng):
                                     ("wide", 8000), ("groups", 300_000)])
 def test_local_fallback_paths(case, n):
     """The stable and LSD local kernels run only when the fast kernel hands
-    segments over (the host reads the fallback counters first): these inputs
+    segments over (srs_debug_last_fallbacks reads the hand-over counts): these inputs
     force each path; the result must equal a stable sort bit for bit."""
     rng = np.random.default_rng(7)
     keys = _fallback_keys(case, n, rng)
     idx = np.arange(n, dtype=np.uint64)
     k, p = keys.copy(), idx.copy()
-    srs_amd.set_kernel_timing(True)
-    srs_amd.reset_kernel_stats()
-    try:
-        srs_amd.sort(k, p)
-        stable_n = srs_amd.kernel_stats("local_stable")[2]
-        lsd_n = srs_amd.kernel_stats("local_lsd")[2]
-    finally:
-        srs_amd.set_kernel_timing(False)
+    srs_amd.sort(k, p)
+    stable_n, lsd_n = srs_amd.last_fallbacks()
     order = np.argsort(keys, kind="stable")
     assert bytes_equal(k, keys[order]) and bytes_equal(p, idx[order])
     if case == "mid64":
@@ -280,6 +274,46 @@ def test_device_inplace_and_out_of_place():
     st = stable_reference(6, True, [kh, p0_in.cpu().numpy(), p1_in.cpu().numpy()])
     assert bytes_equal(ko.cpu().numpy(), st[0])
     assert bytes_equal(o0.cpu().numpy(), st[1]) and bytes_equal(o1.cpu().numpy(), st[2])
+
+
+def test_two_streams_share_the_workspace():
+    """Sorts queued back to back on two non-blocking streams share the
+    device's cached workspace (descriptor, lists, TMP): the second call must
+    wait on the device for the first one's kernels (srs_api.hip WsUse).
+    Three rounds of alternating streams, each result against a stable sort."""
+    torch = _torch()
+    dev = torch.device("cuda:0")
+    streams = [torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev)]
+    sizes = [3_000_000, 2_500_001]
+    ins, outs = [], []
+    for i, n in enumerate(sizes):
+        k = torch.empty(n, dtype=torch.int64, device=dev)
+        p = torch.empty(n, dtype=torch.int64, device=dev)
+        srs_amd.fill_synthetic_device(k, p, seed=1000 + i, key_kind=srs_amd.KEY_U64)
+        ins.append((k, p))
+        outs.append((torch.empty_like(k), torch.empty_like(p)))
+    torch.cuda.synchronize()
+    for _ in range(3):
+        for s, (k, p), (ko, po) in zip(streams, ins, outs):
+            s.wait_stream(torch.cuda.current_stream(dev))  # inputs are ready
+            srs_amd.sort_device(k, p, key_kind=srs_amd.KEY_U64, out=(ko, po), stream=s)
+    torch.cuda.synchronize()
+    for (k, p), (ko, po) in zip(ins, outs):
+        kh, ph = k.cpu().numpy().view(np.uint64), p.cpu().numpy()
+        st = stable_reference(6, True, [kh, ph])
+        assert bytes_equal(ko.cpu().numpy(), st[0]) and bytes_equal(po.cpu().numpy(), st[1])
+
+
+def test_device_api_rejects_mismatched_tensors():
+    torch = _torch()
+    dev = torch.device("cuda:0")
+    k = torch.zeros(100, dtype=torch.int64, device=dev)
+    with pytest.raises(ValueError):
+        srs_amd.sort_device(k, torch.zeros(100, dtype=torch.int64))  # payload on the host
+    with pytest.raises(ValueError):
+        srs_amd.sort_device(k, out=(torch.zeros(99, dtype=torch.int64, device=dev),))
+    with pytest.raises(ValueError):
+        srs_amd.sort_device(k, out=(torch.zeros(100, dtype=torch.int32, device=dev),))
 
 
 def test_device_float_keys_two_payloads():
