@@ -374,6 +374,7 @@ int plan_balanced_level(Workspace* W, const Request& R, const SortDesc& d, bool*
 struct LevelState {
   int64_t nbig, n_local, n_local2, n_copy;
   int cur;
+  int ncols;               // columns moved with the keys (SortDesc::ncols)
   int64_t known_len = -1;  // the length of the single big segment, when the host knows it
 };
 
@@ -471,7 +472,7 @@ int run_level(Workspace* W, int ks, const SortDesc* d_desc, LevelState& S, int f
   {
     TimedScope ts("scatter", (double)0, st);
     launch_scatter(ks, d_desc, plan, tile_seg, (uint64_t*)W->offs.p,
-                   offs32 ? (const uint32_t*)W->offs.p : nullptr, ntiles, lut, st);
+                   offs32 ? (const uint32_t*)W->offs.p : nullptr, ntiles, lut, S.ncols, st);
   }
   HIP_TRY(hipMemcpyAsync(W->h_ctr, d_ctr, sizeof(ListCounters), hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
@@ -613,7 +614,7 @@ int run_sort(Workspace* W, const Request& R, hipStream_t st) {
     n_local2 = (to_local && n > kLocalCapSmall) ? 1 : 0;
     W->h_ctr->local_elems = to_local ? (uint64_t)n : 0;
   }
-  LevelState S{n_big, n_local, n_local2, n_copy, 0};
+  LevelState S{n_big, n_local, n_local2, n_copy, 0, d.ncols};
   if (R.nsegs == 0 && n_big == 1) S.known_len = n;
   int level = 0;
   if (balanced && S.nbig > 0) {
@@ -733,7 +734,7 @@ int run_partition(Workspace* W, const Request& R, int bits, const int32_t* d_lut
                (ListCounters*)W->ctr.p, st);
   int fb = 1;
   while ((1 << fb) < nparts) fb++;
-  LevelState S{1, 0, 0, 0, 0};
+  LevelState S{1, 0, 0, 0, 0, d.ncols};
   SRS_TRY(run_level(W, ks, d_desc, S, fb, true, st));
   // group sizes from the segment's bucket bases (sbase row 0)
   std::vector<uint64_t> sb((size_t)1 << fb);

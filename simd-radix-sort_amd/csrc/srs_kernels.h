@@ -35,7 +35,7 @@ void launch_offsets(SegPlan* plan, int64_t nbig, const int32_t* group_seg, int64
                     const int32_t* lut_rbits, hipStream_t st);
 void launch_scatter(int key_size, const SortDesc* d, const SegPlan* plan,
                     const int32_t* tile_seg, const uint64_t* offs, const uint32_t* offs32,
-                    int64_t ntiles, bool lut, hipStream_t st);
+                    int64_t ntiles, bool lut, int ncols, hipStream_t st);
 void launch_key_hist(int key_size, int64_t n, const void* keys, const SortDesc& d, int bits,
                      unsigned long long* hist, hipStream_t st);
 void launch_local(int key_size, const SortDesc* d, const Seg* segs, int64_t nsegs, int big_class,

@@ -1002,12 +1002,12 @@ struct TileInfo {
   int32_t s;      // segment
 };
 
-template <typename KT, typename U>
+template <typename KT, typename U, bool PRE3>
 __device__ __forceinline__ TileInfo scatter_load_tile(
     const SortDesc* __restrict__ desc, const SegPlan* __restrict__ plan,
     const int32_t* __restrict__ tile_seg, const uint64_t* __restrict__ offs,
     const uint32_t* __restrict__ offs32, int64_t t, int ncols, uint64_t (&v0)[kScatterItems],
-    uint64_t (&v1)[kScatterItems], int64_t& my_off) {
+    uint64_t (&v1)[kScatterItems], uint64_t (&v2)[kScatterItems], int64_t& my_off) {
   constexpr int IT = kScatterItems;
   TileInfo ti;
   ti.s = tile_seg[t];
@@ -1022,6 +1022,9 @@ __device__ __forceinline__ TileInfo scatter_load_tile(
   if (ncols > 1)
     load_strip<IT>(v1, desc->cols[1].base[P.buf], desc->cols[1].width, desc->cols[1].stride,
                    ti.base, ebase, ti.cnt);
+  if (PRE3 && ncols > 2)
+    load_strip<IT>(v2, desc->cols[2].base[P.buf], desc->cols[2].width, desc->cols[2].stride,
+                   ti.base, ebase, ti.cnt);
   my_off = 0;
   if (ti.cnt > 0 && threadIdx.x < (1u << P.bits))
     my_off = offs32 ? (int64_t)offs32[t * kMaxBins + threadIdx.x]
@@ -1029,11 +1032,12 @@ __device__ __forceinline__ TileInfo scatter_load_tile(
   return ti;
 }
 
-template <typename KT, typename U, bool LUT, bool CZ>
+template <typename KT, typename U, bool LUT, bool CZ, bool PRE3>
 __device__ __forceinline__ void scatter_process_tile(
     const SortDesc* __restrict__ desc, const SegPlan* __restrict__ plan, ScatterLds<LUT>& L,
     const TileInfo& ti, int ncols, const uint64_t (&v0)[kScatterItems],
-    uint64_t (&v1)[kScatterItems], int64_t my_off, const DigitLut& lut) {
+    uint64_t (&v1)[kScatterItems], uint64_t (&v2)[kScatterItems], int64_t my_off,
+    const DigitLut& lut) {
   constexpr int NT = kScatterThreads;
   constexpr int IT = kScatterItems;
   constexpr int NW = NT / 64;
@@ -1126,19 +1130,27 @@ __device__ __forceinline__ void scatter_process_tile(
       }
     });
   }
-  // Columns 1..: column c is staged from v1, then column c+1's loads are
-  // issued into the same registers before column c's stores, so their
-  // latency hides behind the stores (no extra VGPRs).
-  for (int c = 1; c < ncols; c++) {
+  // Columns 1..: column c's registers are staged in LDS, then the next
+  // column's loads that use them go out before column c's stores: column
+  // c + 1 (PRE3 = false: one payload register set) or c + 2 (PRE3: three
+  // columns loaded up front, v0, v1, v2). A wave's loads complete in issue
+  // order with its stores (vmcnt counts both), so a load issued after a
+  // store cannot be used before that store is acknowledged; with one set,
+  // column c + 1's loads follow column c - 1's stores and their latency is
+  // partly exposed (C2, three columns: PRE3 scatter 3.53-3.62 -> 3.48 ms).
+  // PRE3 costs 9 VGPRs, which slowed the two-column C3 scatter: it is an
+  // instantiation of its own.
+  constexpr int STEP = PRE3 ? 2 : 1;
+  auto move_col = [&](int c, uint64_t (&v)[IT]) {
     const uint32_t cw = desc->cols[c].width, cst = desc->cols[c].stride;
     lds_barrier();  // every slot of the previous column has been read
 #pragma unroll
     for (int k = 0; k < IT; k++)
-      if (valid(k)) L.sval[pos[k]] = v1[k];
+      if (valid(k)) L.sval[pos[k]] = v[k];
     lds_barrier();
-    if (c + 1 < ncols)
-      load_strip<IT>(v1, desc->cols[c + 1].base[P.buf], desc->cols[c + 1].width,
-                     desc->cols[c + 1].stride, ti.base, ebase, cnt);
+    if (c + STEP < ncols)
+      load_strip<IT>(v, desc->cols[c + STEP].base[P.buf], desc->cols[c + STEP].width,
+                     desc->cols[c + STEP].stride, ti.base, ebase, cnt);
     char* out = desc->cols[c].base[P.dst];
     with_width(cw, [&](auto W_) {
 #pragma unroll
@@ -1149,13 +1161,21 @@ __device__ __forceinline__ void scatter_process_tile(
                                    L.sval[j]);
       }
     });
+  };
+  if constexpr (PRE3) {
+    for (int c = 1; c < ncols; c += 2) {
+      move_col(c, v1);
+      if (c + 1 < ncols) move_col(c + 1, v2);
+    }
+  } else {
+    for (int c = 1; c < ncols; c++) move_col(c, v1);
   }
   STAMP();  // 5: all stores issued (and, in stamp builds, drained)
   STAMP_FLUSH(0);
 }
 
 // One tile per workgroup (XCD-aware order).
-template <typename KT, typename U, bool LUT, bool CZ>
+template <typename KT, typename U, bool LUT, bool CZ, bool PRE3>
 __global__ __launch_bounds__(kScatterThreads, SRS_SCATTER_WAVES_PER_EU) void scatter_kernel(
     const SortDesc* __restrict__ desc, const SegPlan* __restrict__ plan,
     const int32_t* __restrict__ tile_seg, const uint64_t* __restrict__ offs,
@@ -1164,14 +1184,14 @@ __global__ __launch_bounds__(kScatterThreads, SRS_SCATTER_WAVES_PER_EU) void sca
   __shared__ alignas(16) uint16_t slut[LUT ? kLdsLutEntries : 8];
   const int64_t t = xcd_remap(blockIdx.x, gridDim.x);
   const int ncols = desc->ncols;
-  uint64_t v0[kScatterItems], v1[kScatterItems];
+  uint64_t v0[kScatterItems], v1[kScatterItems], v2[kScatterItems];
   int64_t my_off;
-  const TileInfo ti =
-      scatter_load_tile<KT, U>(desc, plan, tile_seg, offs, offs32, t, ncols, v0, v1, my_off);
+  const TileInfo ti = scatter_load_tile<KT, U, PRE3>(desc, plan, tile_seg, offs, offs32, t,
+                                                     ncols, v0, v1, v2, my_off);
   if (ti.cnt == 0) return;
   // (the table is published by the barrier at the top of the tile)
   const DigitLut lut = stage_lut<LUT, kScatterThreads>(desc, slut);
-  scatter_process_tile<KT, U, LUT, CZ>(desc, plan, L, ti, ncols, v0, v1, my_off, lut);
+  scatter_process_tile<KT, U, LUT, CZ, PRE3>(desc, plan, L, ti, ncols, v0, v1, v2, my_off, lut);
 }
 
 // ---------------------------------------------------------------------------
@@ -2195,13 +2215,20 @@ void launch_offsets(SegPlan* plan, int64_t nbig, const int32_t* group_seg, int64
 
 void launch_scatter(int key_size, const SortDesc* d, const SegPlan* plan,
                     const int32_t* tile_seg, const uint64_t* offs, const uint32_t* offs32,
-                    int64_t ntiles, bool lut, hipStream_t st) {
+                    int64_t ntiles, bool lut, int ncols, hipStream_t st) {
+  const bool pre3 = ncols >= 3;
 #define CALL(KT, U, CZ)                                                                 \
-  if (lut)                                                                         \
-    scatter_kernel<KT, U, true, CZ><<<(unsigned)ntiles, kScatterThreads, 0, st>>>(        \
+  if (lut && pre3)                                                                      \
+    scatter_kernel<KT, U, true, CZ, true><<<(unsigned)ntiles, kScatterThreads, 0, st>>>(  \
+        d, plan, tile_seg, offs, offs32);                                               \
+  else if (lut)                                                                         \
+    scatter_kernel<KT, U, true, CZ, false><<<(unsigned)ntiles, kScatterThreads, 0, st>>>( \
+        d, plan, tile_seg, offs, offs32);                                               \
+  else if (pre3)                                                                        \
+    scatter_kernel<KT, U, false, CZ, true><<<(unsigned)ntiles, kScatterThreads, 0, st>>>( \
         d, plan, tile_seg, offs, offs32);                                               \
   else                                                                                  \
-    scatter_kernel<KT, U, false, CZ><<<(unsigned)ntiles, kScatterThreads, 0, st>>>(       \
+    scatter_kernel<KT, U, false, CZ, false><<<(unsigned)ntiles, kScatterThreads, 0, st>>>( \
         d, plan, tile_seg, offs, offs32)
   SRS_KEY_DISPATCH(key_size, CALL)
 #undef CALL
