@@ -30,6 +30,9 @@
 namespace srs {
 namespace {
 
+static_assert(SRS_MAX_COLS >= SRS_MAX_PAYLOADS + 1, "descriptor columns: key + payloads");
+static_assert(sizeof(SortDesc) <= 4096, "SortDesc is a kernel argument (start_kernel)");
+
 thread_local std::string g_err = "no error";
 unsigned long long* g_stamp_acc = nullptr;  // srs_debug_set_stamp_buffer
 
@@ -188,6 +191,7 @@ int ensure_keep(DevBuf& b, size_t bytes, size_t live_bytes, hipStream_t st) {
 
 struct Workspace {
   DevBuf tmp;         // TMP data buffer (same footprint as the input)
+  DevBuf tmp2;        // TMP2: AoS records as SoA slice columns (SortDesc::tmp2)
   DevBuf stage;       // device copy of host arrays (host-pointer API)
   DevBuf desc;        // SortDesc
   DevBuf big[2], local, local2, copy, fallback, fallback2;
@@ -375,6 +379,7 @@ struct LevelState {
   int64_t nbig, n_local, n_local2, n_copy;
   int cur;
   int ncols;               // columns moved with the keys (SortDesc::ncols)
+  int tmp2;                // SortDesc::tmp2
   int64_t known_len = -1;  // the length of the single big segment, when the host knows it
 };
 
@@ -402,12 +407,13 @@ int run_level(Workspace* W, int ks, const SortDesc* d_desc, LevelState& S, int f
   if (small_plan) {
     TimedScope ts("plan", (double)nbig, st);
     launch_plan_small((Seg*)W->big[S.cur].p, nbig, plan, (int64_t*)W->tbase.p,
-                      (int64_t*)W->gbase.p, var, d_totals, &d_ctr->n_big, force_bits, st);
+                      (int64_t*)W->gbase.p, var, d_totals, &d_ctr->n_big, force_bits, S.tmp2,
+                      st);
   } else {
     TimedScope ts("plan", (double)nbig, st);
     HIP_TRY(hipMemsetAsync(d_totals + 3, 0, sizeof(uint64_t), st));
     launch_plan((Seg*)W->big[S.cur].p, nbig, plan, (int64_t*)W->tcount.p,
-                (int64_t*)W->gcount.p, var, d_totals + 3, force_bits, st);
+                (int64_t*)W->gcount.p, var, d_totals + 3, force_bits, S.tmp2, st);
     launch_excl_scan((uint64_t*)W->tcount.p, (uint64_t*)W->tbase.p, nbig,
                      (uint64_t*)W->scan_tmp.p, d_totals + 0, st);
     launch_excl_scan((uint64_t*)W->gcount.p, (uint64_t*)W->gbase.p, nbig,
@@ -503,11 +509,17 @@ int run_sort(Workspace* W, const Request& R, hipStream_t st) {
   d.canon_zero = (is_float && n <= R.thresh) ? 1 : 0;
   const int ksl = ks | (d.canon_zero ? SRS_KS_CANON : 0);  // kernel dispatch key
 
-  size_t tmp_bytes = 0;
+  // AoS records of 16+ bytes travel as SoA slice columns through the
+  // workspace (TMP, TMP2) between the first scatter and the local pass: the
+  // later count passes then read 8-byte keys instead of whole records and
+  // the middle scatters move dense columns
+  const bool aos_cols = R.aos && R.elem_size >= 16 && n > kLocalCap && R.nsegs == 0;
+  size_t tmp_bytes = 0, slice_bytes = 0;
   std::vector<size_t> tmp_off;
   if (R.aos) {
     tmp_off.push_back(0);
-    tmp_bytes = align_up((size_t)n * R.elem_size, 256);
+    slice_bytes = align_up((size_t)n * 8, 256);
+    tmp_bytes = aos_cols ? slice_bytes * (R.elem_size / 8) : align_up((size_t)n * R.elem_size, 256);
   } else {
     for (int c = 0; c < R.ncols; c++) {
       tmp_off.push_back(tmp_bytes);
@@ -516,22 +528,34 @@ int run_sort(Workspace* W, const Request& R, hipStream_t st) {
   }
   SRS_TRY(ensure(W->tmp, tmp_bytes));
   char* tmp = (char*)W->tmp.p;
+  char* tmp2 = nullptr;
+  if (aos_cols) {
+    SRS_TRY(ensure(W->tmp2, tmp_bytes));
+    tmp2 = (char*)W->tmp2.p;
+    d.tmp2 = 1;
+  }
 
   if (R.aos) {
     const uint32_t E = R.elem_size;
     char* in = (char*)R.in_cols[0];
     char* out = (char*)R.out_cols[0];
-    d.key = Col{{in, out, tmp}, (uint32_t)ks, E};
     const uint32_t slice = E < 8 ? E : 8;
     int nc = 0;
-    for (uint32_t off = 0; off < E; off += slice) {
-      d.cols[nc++] = Col{{in + off, out + off, tmp + off}, slice, E};
+    for (uint32_t off = 0; off < E; off += slice, nc++) {
+      if (aos_cols)  // slice nc: a dense 8-byte column in TMP / TMP2
+        d.cols[nc] = Col{{in + off, out + off, tmp + nc * slice_bytes, tmp2 + nc * slice_bytes},
+                         slice, {E, E, 8, 8}};
+      else
+        d.cols[nc] = Col{{in + off, out + off, tmp + off, nullptr}, slice, {E, E, E, E}};
     }
     d.ncols = nc;
+    d.key = d.cols[0];
+    d.key.width = (uint32_t)ks;  // the key: low bytes of slice 0
   } else {
     for (int c = 0; c < R.ncols; c++) {
-      d.cols[c] = Col{{(char*)R.in_cols[c], (char*)R.out_cols[c], tmp + tmp_off[c]},
-                      R.widths[c], R.widths[c]};
+      const uint32_t w = R.widths[c];
+      d.cols[c] = Col{{(char*)R.in_cols[c], (char*)R.out_cols[c], tmp + tmp_off[c], nullptr}, w,
+                      {w, w, w, w}};
     }
     d.key = d.cols[0];
     d.ncols = R.ncols;
@@ -614,7 +638,7 @@ int run_sort(Workspace* W, const Request& R, hipStream_t st) {
     n_local2 = (to_local && n > kLocalCapSmall) ? 1 : 0;
     W->h_ctr->local_elems = to_local ? (uint64_t)n : 0;
   }
-  LevelState S{n_big, n_local, n_local2, n_copy, 0, d.ncols};
+  LevelState S{n_big, n_local, n_local2, n_copy, 0, d.ncols, d.tmp2};
   if (R.nsegs == 0 && n_big == 1) S.known_len = n;
   int level = 0;
   if (balanced && S.nbig > 0) {
@@ -681,7 +705,9 @@ int run_sort(Workspace* W, const Request& R, hipStream_t st) {
     HIP_TRY(hipStreamSynchronize(st));
     TimedScope ts("copy", (double)0, st);
     for (const Seg& g : cp) {
-      if (R.aos) {
+      if (d.tmp2) {  // SoA slice columns back to records
+        launch_copy_home(d_desc, g.start, g.len, g.buf, st);
+      } else if (R.aos) {
         const size_t E = R.elem_size;
         HIP_TRY(hipMemcpyAsync(d.cols[0].base[BUF_OUT] + g.start * E,
                                d.cols[0].base[g.buf] + g.start * E, g.len * E,
@@ -713,7 +739,8 @@ int run_partition(Workspace* W, const Request& R, int bits, const int32_t* d_lut
   for (int c = 0; c < R.ncols; c++) {
     char* in = (char*)R.in_cols[c];
     char* out = (char*)R.out_cols[c];
-    d.cols[c] = Col{{in, out, out}, R.widths[c], R.widths[c]};
+    const uint32_t w = R.widths[c];
+    d.cols[c] = Col{{in, out, out, nullptr}, w, {w, w, w, w}};
   }
   d.key = d.cols[0];
   d.ncols = R.ncols;
@@ -734,7 +761,7 @@ int run_partition(Workspace* W, const Request& R, int bits, const int32_t* d_lut
                (ListCounters*)W->ctr.p, st);
   int fb = 1;
   while ((1 << fb) < nparts) fb++;
-  LevelState S{1, 0, 0, 0, 0, d.ncols};
+  LevelState S{1, 0, 0, 0, 0, d.ncols, 0};
   SRS_TRY(run_level(W, ks, d_desc, S, fb, true, st));
   // group sizes from the segment's bucket bases (sbase row 0)
   std::vector<uint64_t> sb((size_t)1 << fb);
@@ -954,7 +981,7 @@ int srs_fill_synthetic_device(int64_t num, int key_kind, uint64_t seed, uint64_t
     const uint32_t w = payload_sizes[i];
     if (w != 1 && w != 2 && w != 4 && w != 8)
       return fail(SRS_ERR_UNSUPPORTED, "payload sizes must be 1, 2, 4 or 8 bytes");
-    cols[i] = Col{{(char*)payloads[i], nullptr, nullptr}, w, w};
+    cols[i] = Col{{(char*)payloads[i], nullptr, nullptr, nullptr}, w, {w, w, w, w}};
   }
   void* d_cols = nullptr;
   if (num_payloads > 0) {
@@ -1083,7 +1110,7 @@ int srs_release_workspace(void) {
       (void)hipEventSynchronize(w->idle);
       (void)hipEventDestroy(w->idle);
     }
-    DevBuf* bufs[] = {&w->tmp, &w->stage, &w->desc, &w->big[0], &w->big[1], &w->local, &w->local2, &w->fallback, &w->fallback2, &w->shist, &w->lut, &w->lut_rbits,
+    DevBuf* bufs[] = {&w->tmp, &w->tmp2, &w->stage, &w->desc, &w->big[0], &w->big[1], &w->local, &w->local2, &w->fallback, &w->fallback2, &w->shist, &w->lut, &w->lut_rbits,
                       &w->copy, &w->plan, &w->tcount, &w->gcount, &w->tbase, &w->gbase,
                       &w->var, &w->sbase, &w->tile_seg, &w->group_seg, &w->hist, &w->offs,
                       &w->gsum, &w->gofs, &w->scan_tmp, &w->totals, &w->ctr};

@@ -17,18 +17,25 @@
 namespace srs {
 
 // Buffer slots a segment can live in. IN may alias OUT (in-place call).
-enum BufId : int32_t { BUF_IN = 0, BUF_OUT = 1, BUF_TMP = 2 };
+// TMP2: second workspace buffer, used only when AoS records travel as SoA
+// slice columns between the first and the last pass (SortDesc::tmp2).
+enum BufId : int32_t { BUF_IN = 0, BUF_OUT = 1, BUF_TMP = 2, BUF_TMP2 = 3 };
+constexpr int kNumBufs = 4;
 
 // A column of fixed-width elements (the key column, a payload column, or an
 // 8-byte slice of an AoS record). Element i of buffer b lives at
-// base[b] + i * stride, `width` bytes (1, 2, 4 or 8).
+// base[b] + i * stride[b], `width` bytes (1, 2, 4 or 8). The stride depends
+// on the buffer: an AoS slice has the record size in IN / OUT and its own
+// width in the workspace when the workspace holds it as a SoA column.
 struct Col {
-  char* base[3];
-  uint32_t width;
-  uint32_t stride;
+  char* base[kNumBufs];
+  uint32_t width;  // 32-bit fields: scalar loads (a 16-bit field is read with a
+  uint32_t stride[kNumBufs];  // vector load and a vmcnt wait behind the tile's)
 };
 
-#define SRS_MAX_COLS 72
+// the key + 64 payload columns (srs_c_api.h SRS_MAX_PAYLOADS), or <= 8 AoS
+// slices; SortDesc stays under the 4 KB kernel-argument limit
+#define SRS_MAX_COLS 65
 
 // Everything a kernel needs to read keys and move records.
 struct SortDesc {
@@ -38,6 +45,9 @@ struct SortDesc {
   int32_t ncols;
   int32_t key_bits;        // 8 * key size
   int32_t canon_zero;      // float keys, n <= cmpSortThreshold: -0.0 == +0.0
+  int32_t tmp2;            // AoS records as SoA slice columns in TMP / TMP2
+                           // (scatters go IN -> TMP, TMP <-> TMP2; the local
+                           // pass writes the records back to OUT)
   // transformed key u = bits ^ (bits & signbit ? mneg : mpos)
   uint64_t mpos, mneg, signbit, negzero;
   // partition passes only: digit = digit_lut[u >> lut_shift]

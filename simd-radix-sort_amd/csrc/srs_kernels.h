@@ -10,10 +10,11 @@ namespace srs {
 
 void launch_plan(const Seg* big, int64_t nbig, SegPlan* plan, int64_t* tcount,
                  int64_t* gcount, unsigned long long* var_or, uint64_t* elems, int force_bits,
-                 hipStream_t st);
+                 int tmp2, hipStream_t st);
 void launch_plan_small(const Seg* big, int64_t nbig, SegPlan* plan, int64_t* tbase,
                        int64_t* gbase, unsigned long long* var_or, uint64_t* totals,
-                       unsigned long long* n_big_next, int force_bits, hipStream_t st);
+                       unsigned long long* n_big_next, int force_bits, int tmp2,
+                       hipStream_t st);
 constexpr int64_t kPlanSmallMax = 16384;  // plan_small_kernel: one workgroup loops over these
 void launch_seg_map2(const int64_t* tbase, int64_t ntiles, int32_t* tile_seg,
                      const int64_t* gbase, int64_t ngroups, int32_t* group_seg, int64_t nbig,
@@ -52,5 +53,8 @@ bool launch_sample_hist16(const void* keys, int key_bytes, int64_t n, int64_t st
 void launch_fill(int64_t n, int kind, uint64_t seed, uint64_t first, void* keys,
                  int npay, const Col* pays, hipStream_t st);
 void launch_set_desc(const SortDesc& d, SortDesc* out, hipStream_t st);
+// a finished segment in `buf` to OUT, column by column with each buffer's
+// stride (AoS slice columns back into records)
+void launch_copy_home(const SortDesc* d, int64_t start, int64_t len, int buf, hipStream_t st);
 
 }  // namespace srs

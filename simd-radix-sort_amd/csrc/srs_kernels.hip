@@ -102,12 +102,20 @@ __device__ __forceinline__ void store_w(char* p, uint32_t w, uint64_t v) {
 // whose element `first` is at `src`. Dense columns (stride == width) get
 // compile-time per-k offsets (one 64-bit address per strip, immediate
 // offsets after it); strided ones (AoS slices) a multiply per element.
-template <int IT, typename F>
+// DENSE: the caller knows stride == width (no strided code path); FW != 0:
+// the caller knows the width (no width switch: the compiler's vmcnt
+// bookkeeping merges the switch's paths conservatively and then waits for
+// stores issued after the loads it needs)
+template <int IT, bool DENSE = false, int FW = 0, typename F>
 __device__ __forceinline__ void with_strip(uint32_t w, uint32_t st, F&& f) {
-  if (st == w)
+  if constexpr (FW != 0) {
+    static_assert(DENSE, "fixed width implies a dense strip here");
+    f(WidthTag<FW>{}, std::integral_constant<bool, true>{});
+  } else if (DENSE || st == w) {
     with_width(w, [&](auto W_) { f(W_, std::integral_constant<bool, true>{}); });
-  else
+  } else {
     with_width(w, [&](auto W_) { f(W_, std::integral_constant<bool, false>{}); });
+  }
 }
 
 // Buffer resource over `bytes` bytes at `base` (wave-uniform inputs, made
@@ -140,12 +148,12 @@ __device__ __forceinline__ uint64_t bld(__amdgpu_buffer_rsrc_t r, uint32_t voff,
 // and a tile's loads stay in flight together (guarded flat loads of 1/2/4-byte
 // columns were each followed by a full vmcnt(0) wait inside loops; C2
 // 29.9 -> 26.0 ms on the same box). Slots past cnt read 0.
-template <int IT>
+template <int IT, bool DENSE = false, int FW = 0>
 __device__ __forceinline__ void load_strip(uint64_t (&dst)[IT], const char* src, uint32_t w,
                                            uint32_t st, int64_t first, int ebase, int cnt) {
   const __amdgpu_buffer_rsrc_t r =
       strip_rsrc(src + first * (int64_t)st, cnt > 0 ? (uint32_t)cnt * st : 0u);
-  with_strip<IT>(w, st, [&](auto W_, auto D_) {
+  with_strip<IT, DENSE, FW>(w, st, [&](auto W_, auto D_) {
     constexpr int W = decltype(W_)::value;
     constexpr bool D = decltype(D_)::value;
     const uint32_t o0 = (uint32_t)ebase * (D ? (uint32_t)W : st);
@@ -177,12 +185,12 @@ __device__ __forceinline__ void bst(__amdgpu_buffer_rsrc_t r, uint64_t v, uint32
 // Stores slot k of a strip (the layout of load_strip). Range-checked buffer
 // stores: slots past cnt are dropped by the hardware, so value(k) must be
 // safe to evaluate for every k (the caller clamps its LDS indices).
-template <int IT, typename V>
+template <int IT, bool DENSE = false, int FW = 0, typename V>
 __device__ __forceinline__ void store_strip(char* out, uint32_t w, uint32_t st, int64_t first,
                                             int ebase, int cnt, V&& value) {
   const __amdgpu_buffer_rsrc_t r =
       strip_rsrc(out + first * (int64_t)st, cnt > 0 ? (uint32_t)cnt * st : 0u);
-  with_strip<IT>(w, st, [&](auto W_, auto D_) {
+  with_strip<IT, DENSE, FW>(w, st, [&](auto W_, auto D_) {
     constexpr int W = decltype(W_)::value;
     constexpr bool D = decltype(D_)::value;
     const uint32_t o0 = (uint32_t)ebase * (D ? (uint32_t)W : st);
@@ -475,7 +483,7 @@ __device__ __forceinline__ int choose_bits(int64_t len, int rbits) {
   return bits;
 }
 
-__device__ __forceinline__ SegPlan make_plan(const Seg& g, int force_bits) {
+__device__ __forceinline__ SegPlan make_plan(const Seg& g, int force_bits, int tmp2) {
   SegPlan p;
   p.start = g.start;
   p.len = g.len;
@@ -484,7 +492,11 @@ __device__ __forceinline__ SegPlan make_plan(const Seg& g, int force_bits) {
   p.ntiles = (int32_t)((g.len + kTile - 1) / kTile);
   p.ngroups = (p.ntiles + kScanGroup - 1) / kScanGroup;
   p.buf = g.buf;
-  p.dst = (g.buf == BUF_TMP) ? BUF_OUT : BUF_TMP;
+  // the last scatter lands in OUT (the local pass then sorts in place); with
+  // SoA slice columns (tmp2) scatters alternate TMP / TMP2 and the local pass
+  // writes the records home
+  if (tmp2) p.dst = (g.buf == BUF_TMP) ? BUF_TMP2 : BUF_TMP;
+  else p.dst = (g.buf == BUF_TMP) ? BUF_OUT : BUF_TMP;
   p.skip = 0;
   p.tile_base = 0;
   p.group_base = 0;
@@ -495,12 +507,12 @@ __global__ void plan_kernel(const Seg* __restrict__ big, int64_t nbig,
                             SegPlan* __restrict__ plan, int64_t* __restrict__ tcount,
                             int64_t* __restrict__ gcount,
                             unsigned long long* __restrict__ var_or,
-                            uint64_t* __restrict__ elems, int force_bits) {
+                            uint64_t* __restrict__ elems, int force_bits, int tmp2) {
   const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= nbig) return;
   const Seg g = big[s];
   atomicAdd((unsigned long long*)elems, (unsigned long long)g.len);
-  const SegPlan p = make_plan(g, force_bits);
+  const SegPlan p = make_plan(g, force_bits, tmp2);
   plan[s] = p;
   tcount[s] = p.ntiles;
   gcount[s] = p.ngroups;
@@ -517,7 +529,7 @@ __global__ __launch_bounds__(kPlanSmallThreads) void plan_small_kernel(
     const Seg* __restrict__ big, int64_t nbig, SegPlan* __restrict__ plan,
     int64_t* __restrict__ tbase, int64_t* __restrict__ gbase,
     unsigned long long* __restrict__ var_or, uint64_t* __restrict__ totals,
-    unsigned long long* __restrict__ n_big_next, int force_bits) {
+    unsigned long long* __restrict__ n_big_next, int force_bits, int tmp2) {
   constexpr int NT = kPlanSmallThreads;
   __shared__ uint64_t sh[3][NT / 64 + 1];
   uint64_t tc = 0, gc = 0, ec = 0;
@@ -527,7 +539,7 @@ __global__ __launch_bounds__(kPlanSmallThreads) void plan_small_kernel(
     uint64_t nt = 0, ng = 0, len = 0;
     if (s < nbig) {
       const Seg g = big[s];
-      p = make_plan(g, force_bits);
+      p = make_plan(g, force_bits, tmp2);
       nt = (uint64_t)p.ntiles;
       ng = (uint64_t)p.ngroups;
       len = (uint64_t)g.len;
@@ -675,7 +687,7 @@ __global__ __launch_bounds__(kCountThreads) void count_kernel(
   Xform<U, CZ> xf;
   xf.init(*desc);
   const char* kp = desc->key.base[P.buf];
-  const uint32_t ks = desc->key.stride;
+  const uint32_t ks = desc->key.stride[P.buf];
   __shared__ alignas(16) uint16_t slut[LUT ? kLdsLutEntries : 8];
   const DigitLut lut = stage_lut<LUT, kCountThreads>(desc, slut);
 
@@ -1017,14 +1029,14 @@ __device__ __forceinline__ TileInfo scatter_load_tile(
   const int64_t rem = P.len - tl * kTile;
   ti.cnt = P.skip ? 0 : (rem < kTile ? (int)rem : kTile);
   const int ebase = (int)(threadIdx.x >> 6) * IT * 64 + (int)lane_id();
-  load_strip<IT>(v0, desc->cols[0].base[P.buf], desc->cols[0].width, desc->cols[0].stride,
-                 ti.base, ebase, ti.cnt);
+  load_strip<IT>(v0, desc->cols[0].base[P.buf], desc->cols[0].width,
+                 desc->cols[0].stride[P.buf], ti.base, ebase, ti.cnt);
   if (ncols > 1)
-    load_strip<IT>(v1, desc->cols[1].base[P.buf], desc->cols[1].width, desc->cols[1].stride,
-                   ti.base, ebase, ti.cnt);
+    load_strip<IT>(v1, desc->cols[1].base[P.buf], desc->cols[1].width,
+                   desc->cols[1].stride[P.buf], ti.base, ebase, ti.cnt);
   if (PRE3 && ncols > 2)
-    load_strip<IT>(v2, desc->cols[2].base[P.buf], desc->cols[2].width, desc->cols[2].stride,
-                   ti.base, ebase, ti.cnt);
+    load_strip<IT>(v2, desc->cols[2].base[P.buf], desc->cols[2].width,
+                   desc->cols[2].stride[P.buf], ti.base, ebase, ti.cnt);
   my_off = 0;
   if (ti.cnt > 0 && threadIdx.x < (1u << P.bits))
     my_off = offs32 ? (int64_t)offs32[t * kMaxBins + threadIdx.x]
@@ -1113,7 +1125,7 @@ __device__ __forceinline__ void scatter_process_tile(
   uint16_t dout[IT];
   {
     char* out = desc->cols[0].base[P.dst];
-    const uint32_t w = desc->cols[0].width, st = desc->cols[0].stride;
+    const uint32_t w = desc->cols[0].width, st = desc->cols[0].stride[P.dst];
     with_width(w, [&](auto W_) {
 #pragma unroll
       for (int i = 0; i < IT; i++) {
@@ -1142,7 +1154,7 @@ __device__ __forceinline__ void scatter_process_tile(
   // instantiation of its own.
   constexpr int STEP = PRE3 ? 2 : 1;
   auto move_col = [&](int c, uint64_t (&v)[IT]) {
-    const uint32_t cw = desc->cols[c].width, cst = desc->cols[c].stride;
+    const uint32_t cw = desc->cols[c].width, cst = desc->cols[c].stride[P.dst];
     lds_barrier();  // every slot of the previous column has been read
 #pragma unroll
     for (int k = 0; k < IT; k++)
@@ -1150,7 +1162,7 @@ __device__ __forceinline__ void scatter_process_tile(
     lds_barrier();
     if (c + STEP < ncols)
       load_strip<IT>(v, desc->cols[c + STEP].base[P.buf], desc->cols[c + STEP].width,
-                     desc->cols[c + STEP].stride, ti.base, ebase, cnt);
+                     desc->cols[c + STEP].stride[P.buf], ti.base, ebase, cnt);
     char* out = desc->cols[c].base[P.dst];
     with_width(cw, [&](auto W_) {
 #pragma unroll
@@ -1324,16 +1336,21 @@ __global__ __launch_bounds__(NT, WPE) void local_kernel(const SortDesc* __restri
 
   // ---- 1. keys (column 0 holds the key in its low bytes) -------------------
   uint64_t v0[IT];
-  load_strip<IT>(v0, desc->cols[0].base[g.buf], desc->cols[0].width, desc->cols[0].stride, base,
-                 ebase, cnt);
-  const U uref = xf((U)(load_w(desc->cols[0].base[g.buf] + base * (int64_t)desc->cols[0].stride,
+  load_strip<IT>(v0, desc->cols[0].base[g.buf], desc->cols[0].width,
+                 desc->cols[0].stride[g.buf], base, ebase, cnt);
+  const U uref = xf((U)(load_w(desc->cols[0].base[g.buf] +
+                                   base * (int64_t)desc->cols[0].stride[g.buf],
                                desc->cols[0].width) & kmask));
   // keys are recomputed from v0 when needed (holding them costs occupancy)
   auto ukey = [&](int k) -> U { return xf((U)(v0[k] & kmask)); };
   auto valid = [&](int k) -> bool { return ebase + k * 64 < cnt; };
   auto load_col = [&](int c, uint64_t (&dst)[IT]) {
-    load_strip<IT>(dst, desc->cols[c].base[g.buf], desc->cols[c].width, desc->cols[c].stride,
-                   base, ebase, cnt);
+    load_strip<IT>(dst, desc->cols[c].base[g.buf], desc->cols[c].width,
+                   desc->cols[c].stride[g.buf], base, ebase, cnt);
+  };
+  auto load_col_dense = [&](int c, uint64_t (&dst)[IT]) {  // SoA (DIRECT path)
+    load_strip<IT, true>(dst, desc->cols[c].base[g.buf], desc->cols[c].width,
+                         desc->cols[c].stride[g.buf], base, ebase, cnt);
   };
   uint64_t vn[IT];
   U vor = 0;
@@ -1422,8 +1439,11 @@ __global__ __launch_bounds__(NT, WPE) void local_kernel(const SortDesc* __restri
     // it, in the registers v0 frees, forces the rank into quarters: slower).
     // (SoA only: for AoS records the key slice's stores run ahead of the
     // other slices' and C3 measured 11 % slower)
+    // (SoA columns are dense in every buffer: the DIRECT code has no strided
+    // load or store path)
     const bool direct = !CZ && !wide && desc->cols[0].width == (uint32_t)kbytes &&
-                        desc->cols[0].stride == (uint32_t)kbytes;
+                        desc->cols[0].stride[BUF_OUT] == (uint32_t)kbytes && !desc->tmp2 &&
+                        desc->cols[0].stride[BUF_IN] == (uint32_t)kbytes;
     auto bucket_rank = [&](auto DIRECT_) -> bool {
     constexpr bool DIRECT = decltype(DIRECT_)::value;
     // ---- 2. bucket pass on the top varying bits (LDS atomics on 16-bit
@@ -1580,34 +1600,57 @@ __global__ __launch_bounds__(NT, WPE) void local_kernel(const SortDesc* __restri
     };  // bucket_rank
     if (direct) {
       if (bucket_rank(std::true_type{})) return;
-      if (ncols > 1) load_col(1, vn);
       // ---- 4'. column 0 from the words; the rank left each output slot's
       // word slot in perm. u = known top bits | word bits, then the inverse
-      // key transform. The other columns as below (staged, written in order).
-      uint32_t id[IT];
-      const uint64_t top = (uint64_t)uref & ~keep;
-      const uint64_t imask = (1u << IDXB) - 1;
-      store_strip<IT>(desc->cols[0].base[BUF_OUT], desc->cols[0].width, desc->cols[0].stride,
-                      base, ebase, cnt, [&](int k) -> uint64_t {
-                        const int e = ebase + k * 64;
-                        const uint64_t w = sbuf[perm[e < cnt ? e : 0]];
-                        id[k] = (uint32_t)(w & imask);
-                        return (uint64_t)xf.inv((U)(top | (w >> IDXB)));
-                      });
-      STAMP();  // 5: column 0 moved
-      for (int c = 1; c < ncols; c++) {
-        uint64_t v[IT];
+      // key transform. The other columns staged, written in order. FW: the
+      // payload width as a compile-time fact for the common one-column case.
+      auto direct_out = [&](auto FW_) {
+        constexpr int FW = decltype(FW_)::value;
+        if (ncols > 1) {
+          if constexpr (FW != 0) load_strip<IT, true, FW>(vn, desc->cols[1].base[g.buf], FW, FW,
+                                                          base, ebase, cnt);
+          else load_col_dense(1, vn);
+        }
+        uint32_t id[IT];
+        const uint64_t top = (uint64_t)uref & ~keep;
+        const uint64_t imask = (1u << IDXB) - 1;
+        // (column 0 is the key column: its width is sizeof(KT))
+        store_strip<IT, true, (int)sizeof(KT)>(desc->cols[0].base[BUF_OUT], desc->cols[0].width,
+                              desc->cols[0].stride[BUF_OUT], base, ebase, cnt,
+                              [&](int k) -> uint64_t {
+                                const int e = ebase + k * 64;
+                                const uint64_t w = sbuf[perm[e < cnt ? e : 0]];
+                                id[k] = (uint32_t)(w & imask);
+                                return (uint64_t)xf.inv((U)(top | (w >> IDXB)));
+                              });
+        STAMP();  // 5: column 0 moved
+        if constexpr (FW != 0) {  // exactly one payload column
+          lds_barrier();  // every read of the words is done
 #pragma unroll
-        for (int k = 0; k < IT; k++) v[k] = vn[k];
-        if (c + 1 < ncols) load_col(c + 1, vn);
-        lds_barrier();  // every read of sbuf (words, or the previous column) is done
+          for (int k = 0; k < IT; k++)
+            if (valid(k)) sbuf[ebase + k * 64] = vn[k];
+          lds_barrier();
+          store_strip<IT, true, FW>(desc->cols[1].base[BUF_OUT], FW, FW, base, ebase, cnt,
+                                    [&](int k) { return sbuf[id[k]]; });
+        } else {
+          // column c is staged straight from vn, whose registers then take
+          // column c + 1's loads before column c's stores (no register
+          // copies: a copy of in-flight load results costs a vmcnt(0) wait)
+          for (int c = 1; c < ncols; c++) {
+            lds_barrier();  // every read of sbuf (words, or the previous column) is done
 #pragma unroll
-        for (int k = 0; k < IT; k++)
-          if (valid(k)) sbuf[ebase + k * 64] = v[k];
-        lds_barrier();
-        store_strip<IT>(desc->cols[c].base[BUF_OUT], desc->cols[c].width, desc->cols[c].stride,
-                        base, ebase, cnt, [&](int k) { return sbuf[id[k]]; });
-      }
+            for (int k = 0; k < IT; k++)
+              if (valid(k)) sbuf[ebase + k * 64] = vn[k];
+            if (c + 1 < ncols) load_col_dense(c + 1, vn);
+            lds_barrier();
+            store_strip<IT, true>(desc->cols[c].base[BUF_OUT], desc->cols[c].width,
+                                  desc->cols[c].stride[BUF_OUT], base, ebase, cnt,
+                                  [&](int k) { return sbuf[id[k]]; });
+          }
+        }
+      };
+      if (ncols == 2 && desc->cols[1].width == 8) direct_out(std::integral_constant<int, 8>{});
+      else direct_out(std::integral_constant<int, 0>{});
       STAMP();  // 6
       STAMP_FLUSH(1);
       return;
@@ -1632,22 +1675,30 @@ __global__ __launch_bounds__(NT, WPE) void local_kernel(const SortDesc* __restri
   // safe: a column's loads complete before the barrier that precedes its own
   // stores, and different columns never share bytes.
   if (ncols > 1) load_col(1, vn);
-  for (int c = 0; c < ncols; c++) {
-    uint64_t v[IT];
+  // column 0 from v0 (the barrier after the perm writes already ordered
+  // every earlier sbuf access), then each column c >= 1 staged straight from
+  // vn, whose registers take column c + 1's loads before column c's stores
+  // (no register copies: a copy of in-flight load results waits vmcnt(0))
 #pragma unroll
-    for (int k = 0; k < IT; k++) v[k] = c == 0 ? v0[k] : vn[k];
-    if (c >= 1 && c + 1 < ncols) load_col(c + 1, vn);
-    // previous users of sbuf are done (for c == 0 the barrier after the perm
-    // writes already ordered every earlier sbuf access)
-    if (c > 0) lds_barrier();
+  for (int k = 0; k < IT; k++)
+    if (valid(k)) sbuf[ebase + k * 64] = v0[k];
+  lds_barrier();
+  store_strip<IT>(desc->cols[0].base[BUF_OUT], desc->cols[0].width,
+                  desc->cols[0].stride[BUF_OUT], base, ebase, cnt,
+                  [&](int k) { return sbuf[id[k]]; });
+  STAMP();  // 5: column 0 moved
+  for (int c = 1; c < ncols; c++) {
+    lds_barrier();
 #pragma unroll
     for (int k = 0; k < IT; k++)
-      if (valid(k)) sbuf[ebase + k * 64] = v[k];
+      if (valid(k)) sbuf[ebase + k * 64] = vn[k];
+    if (c + 1 < ncols) load_col(c + 1, vn);
     lds_barrier();
-    store_strip<IT>(desc->cols[c].base[BUF_OUT], desc->cols[c].width, desc->cols[c].stride, base,
-                    ebase, cnt, [&](int k) { return sbuf[id[k]]; });
-    STAMP();  // 5, 6: column moved
+    store_strip<IT>(desc->cols[c].base[BUF_OUT], desc->cols[c].width,
+                    desc->cols[c].stride[BUF_OUT], base, ebase, cnt,
+                    [&](int k) { return sbuf[id[k]]; });
   }
+  STAMP();  // 6: columns moved
   STAMP_FLUSH(1);
 }
 
@@ -1706,7 +1757,7 @@ __global__ __launch_bounds__(NT) void local_stable_kernel(
   uint64_t v0[IT];
   {
     const char* src = desc->cols[0].base[g.buf];
-    const uint32_t w = desc->cols[0].width, st = desc->cols[0].stride;
+    const uint32_t w = desc->cols[0].width, st = desc->cols[0].stride[g.buf];
 with_width(w, [&](auto W_) {
 #pragma unroll
   for (int k = 0; k < IT; k++) {
@@ -1715,7 +1766,8 @@ with_width(w, [&](auto W_) {
   }
 });
   }
-  const U uref = xf((U)(load_w(desc->cols[0].base[g.buf] + base * (int64_t)desc->cols[0].stride,
+  const U uref = xf((U)(load_w(desc->cols[0].base[g.buf] +
+                                   base * (int64_t)desc->cols[0].stride[g.buf],
                                desc->cols[0].width) & kmask));
   // keys are recomputed from v0 when needed (holding them costs occupancy)
   auto ukey = [&](int k) -> U { return xf((U)(v0[k] & kmask)); };
@@ -1899,7 +1951,7 @@ with_width(w, [&](auto W_) {
   // ---- 5. columns, software-pipelined as in local_kernel -------------------
   auto load_col = [&](int c, uint64_t (&dst)[IT]) {
     const char* src = desc->cols[c].base[g.buf];
-    const uint32_t st = desc->cols[c].stride;
+    const uint32_t st = desc->cols[c].stride[g.buf];
     with_width(desc->cols[c].width, [&](auto W_) {
 #pragma unroll
       for (int k = 0; k < IT; k++) {
@@ -1912,7 +1964,7 @@ with_width(w, [&](auto W_) {
   load_col(0, vn);  // (the keys are reloaded: keeping them costs occupancy)
   for (int c = 0; c < ncols; c++) {
     char* out = desc->cols[c].base[BUF_OUT];
-    const uint32_t st = desc->cols[c].stride;
+    const uint32_t st = desc->cols[c].stride[BUF_OUT];
     uint64_t v[IT];
 #pragma unroll
     for (int k = 0; k < IT; k++) v[k] = vn[k];
@@ -1972,7 +2024,7 @@ __global__ __launch_bounds__(kLocalStableThreads) void local_lsd_kernel(
     bool valid[IT];
     {
       const char* src = desc->cols[0].base[g.buf];
-      const uint32_t w = desc->cols[0].width, st = desc->cols[0].stride;
+      const uint32_t w = desc->cols[0].width, st = desc->cols[0].stride[g.buf];
       with_width(w, [&](auto W_) {
 #pragma unroll
         for (int k = 0; k < IT; k++) {
@@ -1985,7 +2037,8 @@ __global__ __launch_bounds__(kLocalStableThreads) void local_lsd_kernel(
       });
     }
     __syncthreads();
-    const U uref = xf((U)(load_w(desc->cols[0].base[g.buf] + base * (int64_t)desc->cols[0].stride,
+    const U uref = xf((U)(load_w(desc->cols[0].base[g.buf] +
+                                     base * (int64_t)desc->cols[0].stride[g.buf],
                                  desc->cols[0].width) & kmask));
     U vor = 0;
 #pragma unroll
@@ -2015,12 +2068,13 @@ __global__ __launch_bounds__(kLocalStableThreads) void local_lsd_kernel(
     for (int c = 0; c < ncols; c++) {
       const char* src = desc->cols[c].base[g.buf];
       char* out = desc->cols[c].base[BUF_OUT];
-      const uint32_t w = desc->cols[c].width, st = desc->cols[c].stride;
+      const uint32_t w = desc->cols[c].width, st = desc->cols[c].stride[BUF_OUT];
+      const uint32_t sti = desc->cols[c].stride[g.buf];
       uint64_t v[IT];
       with_width(w, [&](auto W_) {
 #pragma unroll
         for (int k = 0; k < IT; k++)
-          v[k] = valid[k] ? ldw<decltype(W_)::value>(src + (base + (int64_t)id[k]) * st) : 0;
+          v[k] = valid[k] ? ldw<decltype(W_)::value>(src + (base + (int64_t)id[k]) * sti) : 0;
       });
       __syncthreads();
       with_width(w, [&](auto W_) {
@@ -2148,16 +2202,17 @@ __global__ void fill_kernel(int64_t n, int kind, uint64_t seed, uint64_t first,
 
 void launch_plan(const Seg* big, int64_t nbig, SegPlan* plan, int64_t* tcount,
                  int64_t* gcount, unsigned long long* var_or, uint64_t* elems, int force_bits,
-                 hipStream_t st) {
-  plan_kernel<<<(unsigned)((nbig + 255) / 256), 256, 0, st>>>(big, nbig, plan, tcount,
-                                                              gcount, var_or, elems, force_bits);
+                 int tmp2, hipStream_t st) {
+  plan_kernel<<<(unsigned)((nbig + 255) / 256), 256, 0, st>>>(
+      big, nbig, plan, tcount, gcount, var_or, elems, force_bits, tmp2);
 }
 
 void launch_plan_small(const Seg* big, int64_t nbig, SegPlan* plan, int64_t* tbase,
                        int64_t* gbase, unsigned long long* var_or, uint64_t* totals,
-                       unsigned long long* n_big_next, int force_bits, hipStream_t st) {
+                       unsigned long long* n_big_next, int force_bits, int tmp2,
+                       hipStream_t st) {
   plan_small_kernel<<<1, kPlanSmallThreads, 0, st>>>(big, nbig, plan, tbase, gbase, var_or,
-                                                     totals, n_big_next, force_bits);
+                                                     totals, n_big_next, force_bits, tmp2);
 }
 
 void launch_plan_bases(SegPlan* plan, int64_t nbig, const int64_t* tbase,
@@ -2331,6 +2386,28 @@ __device__ __forceinline__ void init_lists_body(Seg seg0, int to_local, Seg* big
   }
 }
 
+
+// One finished segment home: element i of every column from `buf` (its
+// stride there) to OUT (its stride there).
+__global__ __launch_bounds__(256) void copy_home_kernel(const SortDesc* __restrict__ desc,
+                                                        int64_t start, int64_t len, int buf) {
+  const int ncols = desc->ncols;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < len;
+       i += (int64_t)gridDim.x * 256) {
+    const int64_t e = start + i;
+    for (int c = 0; c < ncols; c++) {
+      const Col& C = desc->cols[c];
+      store_w(C.base[BUF_OUT] + e * (int64_t)C.stride[BUF_OUT], C.width,
+              load_w(C.base[buf] + e * (int64_t)C.stride[buf], C.width));
+    }
+  }
+}
+
+void launch_copy_home(const SortDesc* d, int64_t start, int64_t len, int buf, hipStream_t st) {
+  if (len <= 0) return;
+  const int64_t blocks = std::min<int64_t>((len + 255) / 256, 8192);
+  copy_home_kernel<<<(unsigned)blocks, 256, 0, st>>>(d, start, len, buf);
+}
 
 void launch_set_desc(const SortDesc& d, SortDesc* out, hipStream_t st) {
   set_desc_kernel<<<1, 64, 0, st>>>(d, out);

@@ -250,6 +250,29 @@ def test_combined_records(kind, esz_mult, up):
         assert bytes_equal(e[:, :ks], o[:, :ks])
 
 
+@pytest.mark.parametrize("esz,n,case", [(16, 4_000_003, "uniform"), (32, 3_500_000, "uniform"),
+                                        (64, 3_300_001, "gaussian"), (16, 200_000, "dupblock"),
+                                        (32, 150_000, "dupblock")])
+def test_combined_records_slice_columns(esz, n, case):
+    """Records of 16+ bytes travel as SoA slice columns through TMP / TMP2
+    between the first scatter and the local pass (SortDesc::tmp2): two
+    global levels (n > 3.1M) use both workspace buffers; 'dupblock' puts 40 %
+    of the records on one key, a finished segment larger than the local
+    capacity that is copied home column by column (copy_home_kernel)."""
+    kind = 7  # int64 keys
+    rng = np.random.default_rng(n + esz)
+    if case == "dupblock":
+        keys = rng.integers(-2**62, 2**62, n, dtype=np.int64)
+        keys[rng.random(n) < 0.4] = 123456789
+    else:
+        keys = make_keys(kind, case, n, esz)
+    elems = rng.integers(0, 256, (n, esz), dtype=np.uint8)
+    elems[:, :8] = keys.view(np.uint8).reshape(n, 8)
+    e = elems.copy()
+    srs_amd.sort_combined(e, kind)
+    assert bytes_equal(e, stable_aos(kind, True, elems))
+
+
 # ---------------------------------------------------------------------------
 # device API (torch tensors in HBM)
 # ---------------------------------------------------------------------------
