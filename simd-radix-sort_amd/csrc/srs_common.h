@@ -161,5 +161,12 @@ constexpr int kLocalStableThreadsSmall = kLocalCapSmall / kLocalStableItems;
 static_assert(kLocalStableThreads * kLocalStableItems == kLocalCap, "fallback capacity");
 static_assert(kLocalStableThreadsSmall * kLocalStableItems == kLocalCapSmall, "fallback capacity");
 constexpr int kLocalTarget = 6144;                        // digit sizing target
+// average bucket that still lands in the small class: ~94 % full for uniform
+// keys (the small class is 2.5x cheaper per key than the large one, and a
+// half-empty small segment costs ~1.5x per key of a full one)
+#ifndef SRS_LOCAL_SMALL_TARGET
+#define SRS_LOCAL_SMALL_TARGET 3840
+#endif
+constexpr int kLocalSmallTarget = SRS_LOCAL_SMALL_TARGET;
 
 }  // namespace srs

@@ -474,7 +474,7 @@ __device__ __forceinline__ int choose_bits(int64_t len, int rbits) {
   // the buckets in the smaller (faster) LDS class without an extra level
   int need, need_small;
   const int levels = levels_for(len, kLocalTarget, &need);
-  const int levels_small = levels_for(len, kLocalTarget / 2, &need_small);
+  const int levels_small = levels_for(len, kLocalSmallTarget, &need_small);
   if (levels_small == levels) need = need_small;
   int bits = (need + levels - 1) / levels;
   if (bits > kMaxDigitBits) bits = kMaxDigitBits;

@@ -5,6 +5,7 @@ import sys
 
 KEEP = ("count", "scatter", "local", "local_fast", "local_stable", "scan")
 for path in sys.argv[1:]:
+    path = "/dev/stdin" if path == "-" else path
     line = None
     try:
         with open(path) as f:
