@@ -53,7 +53,48 @@ def parse():
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--shard", action="store_true",
                     help="run the multi-GPU shard protocol even at one rank (RCCL, world 1)")
+    ap.add_argument("--dist", default="uniform", choices=DISTS,
+                    help="key distribution (the reference's InputDistribution kinds, "
+                         "src/data.hpp:64-73; c1 only; payload = f(key) as always)")
     return ap.parse_args()
+
+
+DISTS = ("uniform", "gaussian", "zero", "zeroone", "sorted", "reverse", "almostsorted",
+         "almostreverse")
+
+
+def make_dist_keys(keys, pays, dist, torch, srs_amd, kind):
+    """Replaces the uniform keys of a c1 workload (int64 storage of u64 keys)
+    by the reference's InputDistribution `dist` (src/data.hpp:115-160):
+    Gaussian = round(N(0, 100)); Zero; ZeroOne; Sorted / ReverseSorted =
+    uniform, sorted; Almost* = that plus 2^log10(n) random swaps. Sorting
+    uses this library (the input of the timed sort is then its own output).
+    Payloads are recomputed as f(key)."""
+    import math
+    n = keys.numel()
+    g = torch.Generator(device=keys.device)
+    g.manual_seed(42)
+    if dist == "gaussian":
+        keys.copy_(torch.round(torch.randn(n, device=keys.device, generator=g) * 100).to(torch.int64))
+    elif dist == "zero":
+        keys.zero_()
+    elif dist == "zeroone":
+        keys.copy_(torch.randint(0, 2, (n,), device=keys.device, generator=g))
+    elif dist in ("sorted", "reverse", "almostsorted", "almostreverse"):
+        srs_amd.sort_device(keys, key_kind=kind, up=dist in ("sorted", "almostsorted"))
+        if dist.startswith("almost"):
+            m = int(2 ** math.log10(n))
+            a = torch.randint(0, n, (m,), device=keys.device, generator=g)
+            b = torch.randint(0, n, (m,), device=keys.device, generator=g)
+            for i, j in zip(a.tolist(), b.tolist()):  # sequential swaps, as the reference
+                ki, kj = keys[i].clone(), keys[j].clone()
+                keys[i], keys[j] = kj, ki
+    for c, p in enumerate(pays):
+        salt = (c * 0xD1B54A32D192ED03) & ((1 << 64) - 1)
+        salt = salt - (1 << 64) if salt >= 1 << 63 else salt
+        for i in range(0, n, 1 << 26):
+            f = _splitmix64(_u64_bits(keys[i:i + (1 << 26)], torch) ^ salt, torch)
+            p[i:i + (1 << 26)].copy_(f if p.element_size() == 8 else (f & 0xFFFFFFFF).to(p.dtype))
 
 
 def pmc_traffic(kernel, workload, n):
@@ -177,6 +218,10 @@ def main():
     keys = torch.empty(n, dtype=key_dt, device=dev)
     pays = [torch.empty(n, dtype=tdt[s], device=dev) for s in psizes]
     srs_amd.fill_synthetic_device(keys, *pays, seed=42 << 32, first_index=rank * n, key_kind=kind)
+    if args.dist != "uniform":
+        if args.config != "c1":
+            raise SystemExit("--dist applies to c1 (u64 keys + u64 payload)")
+        make_dist_keys(keys, pays, args.dist, torch, srs_amd, kind)
     rec = rec_out = None
     if layout == "aos":
         rec = torch.stack([keys, pays[0]], dim=1).contiguous()
@@ -302,7 +347,8 @@ def main():
             "vs_baseline": None,
             "dtype": kname if kname != "u64" else "uint64",
             "data": "synthetic (device splitmix64 of the global index; payload = f(key))",
-            "config": {"workload": args.config + ": " + cdesc, "keys_per_gpu": n,
+            "config": {"workload": args.config + ": " + cdesc +
+                       ("" if args.dist == "uniform" else f", {args.dist} keys"), "keys_per_gpu": n,
                        "total_keys": n * world, "record_bytes": rec_bytes,
                        "parallelism": f"top-radix-bits shard x{world}" if world > 1 else "1 GPU"},
             "roofline": roofline,

@@ -343,6 +343,22 @@ int plan_balanced_level(Workspace* W, const Request& R, const SortDesc& d, bool*
     last[g] = b;
     before += h[b];
   }
+  // the table only pays when its groups outnumber the plain digit's
+  // non-empty buckets (Gaussian int64 keys fill two 16-bit bins: both ways
+  // give two buckets, and the table pass is the slower one)
+  int groups_used = 0, buckets_used = 0;
+  {
+    std::vector<uint8_t> has(kGroups, 0);
+    for (int b = 0; b < 65536; b++)
+      if (h[b]) has[lut[b]] = 1;
+    for (int g = 0; g < kGroups; g++) groups_used += has[g];
+  }
+  for (int b = 0; b < 512; b++) {
+    bool any = false;
+    for (int j = 0; j < 128 && !any; j++) any = h[b * 128 + j] != 0;
+    buckets_used += any;
+  }
+  if (groups_used < 2 * buckets_used) return SRS_OK;
   for (int g = 0; g < kGroups; g++) {
     const int diff = first[g] < 0 ? 0xFFFF : (first[g] ^ last[g]);
     int bl = 0;
@@ -699,28 +715,16 @@ int run_sort(Workspace* W, const Request& R, hipStream_t st) {
     }
   }
   if (n_copy > 0) {
+    // the list stays on the device; only the longest length sizes the grid
+    // (a read-back the plain uniform case never pays: its copy list is empty)
     std::vector<Seg> cp((size_t)n_copy);
     HIP_TRY(hipMemcpyAsync(cp.data(), W->copy.p, n_copy * sizeof(Seg),
                            hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
+    int64_t max_len = 0;
+    for (const Seg& g : cp) max_len = std::max<int64_t>(max_len, g.len);
     TimedScope ts("copy", (double)0, st);
-    for (const Seg& g : cp) {
-      if (d.tmp2) {  // SoA slice columns back to records
-        launch_copy_home(d_desc, g.start, g.len, g.buf, st);
-      } else if (R.aos) {
-        const size_t E = R.elem_size;
-        HIP_TRY(hipMemcpyAsync(d.cols[0].base[BUF_OUT] + g.start * E,
-                               d.cols[0].base[g.buf] + g.start * E, g.len * E,
-                               hipMemcpyDeviceToDevice, st));
-      } else {
-        for (int c = 0; c < d.ncols; c++) {
-          const size_t w = d.cols[c].width;
-          HIP_TRY(hipMemcpyAsync(d.cols[c].base[BUF_OUT] + g.start * w,
-                                 d.cols[c].base[g.buf] + g.start * w, g.len * w,
-                                 hipMemcpyDeviceToDevice, st));
-        }
-      }
-    }
+    launch_copy_list(d_desc, (const Seg*)W->copy.p, n_copy, max_len, st);
   }
   HIP_TRY(hipGetLastError());
   return SRS_OK;

@@ -53,8 +53,9 @@ bool launch_sample_hist16(const void* keys, int key_bytes, int64_t n, int64_t st
 void launch_fill(int64_t n, int kind, uint64_t seed, uint64_t first, void* keys,
                  int npay, const Col* pays, hipStream_t st);
 void launch_set_desc(const SortDesc& d, SortDesc* out, hipStream_t st);
-// a finished segment in `buf` to OUT, column by column with each buffer's
-// stride (AoS slice columns back into records)
-void launch_copy_home(const SortDesc* d, int64_t start, int64_t len, int buf, hipStream_t st);
+// the copy list (finished segments not in OUT) home in one launch, column by
+// column with each buffer's stride (AoS slice columns back into records)
+void launch_copy_list(const SortDesc* d, const Seg* segs, int64_t nsegs, int64_t max_len,
+                      hipStream_t st);
 
 }  // namespace srs

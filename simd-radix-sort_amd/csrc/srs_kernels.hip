@@ -706,14 +706,33 @@ __global__ __launch_bounds__(kCountThreads) void count_kernel(
     raw[k] = e < cnt ? (U)gld<KT>(kp + (base + e) * (int64_t)ks) : (U)0;
   }
   U vor = 0;
+  // A wave holds 64 consecutive keys. Sorted or constant inputs give it one
+  // digit, and 64 lanes adding into one LDS counter serialise (sorted C1
+  // input: 3.6 ms per count launch against 1.45 uniform). A wave whose valid
+  // lanes all share one digit adds once. Whether to look is decided once per
+  // tile from the first item (the per-item check cost C2's 4-byte count 9 %).
+  bool agg;
+  {
+    const uint32_t d = pass_digit<LUT>(xf(raw[0]), P.shift, mask, lut);
+    const uint32_t d0 = __builtin_amdgcn_readfirstlane(d);
+    agg = __ballot(threadIdx.x < (uint32_t)cnt && d == d0) == __ballot(threadIdx.x < (uint32_t)cnt);
+  }
 #pragma unroll
   for (int k = 0; k < kCountItems; k++) {
     const int e = k * kCountThreads + threadIdx.x;
-    if (e < cnt) {
-      const U u = xf(raw[k]);
-      atomicAdd(&h[pass_digit<LUT>(u, P.shift, mask, lut)], 1u);
-      vor |= u ^ uref;
+    const bool ok = e < cnt;
+    const U u = xf(raw[k]);
+    const uint32_t d = pass_digit<LUT>(u, P.shift, mask, lut);
+    if (ok) vor |= u ^ uref;
+    if (agg) {
+      const uint32_t d0 = __builtin_amdgcn_readfirstlane(d);
+      const uint64_t valid = __ballot(ok);
+      if (__ballot(ok && d == d0) == valid) {
+        if (valid && lane_id() == 0) atomicAdd(&h[d0], (uint32_t)__popcll(valid));
+        continue;
+      }
     }
+    if (ok) atomicAdd(&h[d], 1u);
   }
   if (vor) atomicOr(&sh_or, (unsigned long long)vor);
   __syncthreads();
@@ -2387,26 +2406,39 @@ __device__ __forceinline__ void init_lists_body(Seg seg0, int to_local, Seg* big
 }
 
 
-// One finished segment home: element i of every column from `buf` (its
-// stride there) to OUT (its stride there).
-__global__ __launch_bounds__(256) void copy_home_kernel(const SortDesc* __restrict__ desc,
-                                                        int64_t start, int64_t len, int buf) {
+// Finished segments home: every segment of the copy list (finished, not in
+// OUT) is moved to OUT in one launch, column by column with each buffer's
+// stride. blockIdx.y picks the segment, blockIdx.x strides over it. (A
+// hipMemcpyAsync per segment and column cost ~5 us each: duplicate-heavy
+// inputs finish hundreds of large segments at once.)
+__global__ __launch_bounds__(256) void copy_list_kernel(const SortDesc* __restrict__ desc,
+                                                        const Seg* __restrict__ segs) {
+  const Seg g = segs[blockIdx.y];
   const int ncols = desc->ncols;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < len;
-       i += (int64_t)gridDim.x * 256) {
-    const int64_t e = start + i;
-    for (int c = 0; c < ncols; c++) {
-      const Col& C = desc->cols[c];
-      store_w(C.base[BUF_OUT] + e * (int64_t)C.stride[BUF_OUT], C.width,
-              load_w(C.base[buf] + e * (int64_t)C.stride[buf], C.width));
-    }
+  for (int c = 0; c < ncols; c++) {
+    const Col& C = desc->cols[c];
+    const uint32_t si = C.stride[g.buf], so = C.stride[BUF_OUT];
+    const char* src = C.base[g.buf] + g.start * (int64_t)si;
+    char* dst = C.base[BUF_OUT] + g.start * (int64_t)so;
+    with_width(C.width, [&](auto W_) {
+      constexpr int W = decltype(W_)::value;
+      for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < g.len;
+           i += (int64_t)gridDim.x * 256)
+        stw<W>(dst + i * so, ldw<W>(src + i * si));
+    });
   }
 }
 
-void launch_copy_home(const SortDesc* d, int64_t start, int64_t len, int buf, hipStream_t st) {
-  if (len <= 0) return;
-  const int64_t blocks = std::min<int64_t>((len + 255) / 256, 8192);
-  copy_home_kernel<<<(unsigned)blocks, 256, 0, st>>>(d, start, len, buf);
+void launch_copy_list(const SortDesc* d, const Seg* segs, int64_t nsegs, int64_t max_len,
+                      hipStream_t st) {
+  if (nsegs <= 0) return;
+  // ~4096 blocks in all, at most one per 256 elements of the longest segment
+  const int64_t per = std::max<int64_t>(1, std::min<int64_t>((max_len + 255) / 256,
+                                                             (4096 + nsegs - 1) / nsegs));
+  for (int64_t s0 = 0; s0 < nsegs; s0 += 65535) {  // grid.y limit
+    const unsigned ny = (unsigned)std::min<int64_t>(65535, nsegs - s0);
+    copy_list_kernel<<<dim3((unsigned)per, ny), 256, 0, st>>>(d, segs + s0);
+  }
 }
 
 void launch_set_desc(const SortDesc& d, SortDesc* out, hipStream_t st) {
