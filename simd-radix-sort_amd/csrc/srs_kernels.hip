@@ -487,8 +487,11 @@ __device__ __forceinline__ SegPlan make_plan(const Seg& g, int force_bits, int t
   SegPlan p;
   p.start = g.start;
   p.len = g.len;
-  p.bits = force_bits ? force_bits : choose_bits(g.len, g.rbits);
-  p.shift = force_bits ? g.rbits : g.rbits - p.bits;  // LUT levels consume no fixed bits
+  // force_bits > 0: a digit-table level (consumes no fixed bits); < 0: a
+  // plain digit of -force_bits bits (a partition whose groups are aligned
+  // top-bit ranges)
+  p.bits = force_bits ? (force_bits > 0 ? force_bits : -force_bits) : choose_bits(g.len, g.rbits);
+  p.shift = force_bits > 0 ? g.rbits : g.rbits - p.bits;
   p.ntiles = (int32_t)((g.len + kTile - 1) / kTile);
   p.ngroups = (p.ntiles + kScanGroup - 1) / kScanGroup;
   p.buf = g.buf;

@@ -398,8 +398,14 @@ def test_key_histogram_and_partition(kind):
     u = transformed_keys(kind, True, keys_h)
     top = (u >> np.uint64(8 * key_size(kind) - bits)).astype(np.int64)
     assert np.array_equal(hist.cpu().numpy(), np.bincount(top, minlength=1 << bits))
-    for world in (1, 3, 8):
-        pob = balanced_split(hist, world)
+    aligned = {8: torch.arange(1 << bits, dtype=torch.int32, device="cuda") >> (bits - 3),
+               512: torch.arange(1 << bits, dtype=torch.int32, device="cuda") >> (bits - 9)}
+    for world in (1, 3, 8, "a8", "a512"):
+        if isinstance(world, str):  # groups = top-bit ranges: the plain-digit partition
+            world = int(world[1:])
+            pob = aligned[world]
+        else:
+            pob = balanced_split(hist, world)
         ko, po = torch.empty_like(keys), torch.empty_like(pay)
         counts = srs_amd.partition_device(keys, [pay], bits, pob, world, (ko, po), key_kind=kind)
         dest = pob.cpu().numpy()[top]
