@@ -104,6 +104,9 @@ struct ListCounters {
 #ifndef SRS_SCATTER_WAVES_PER_EU
 #define SRS_SCATTER_WAVES_PER_EU 8
 #endif
+#ifndef SRS_SCATTER_SDIG
+#define SRS_SCATTER_SDIG 1   // stage each slot's digit (0: recompute it from the key)
+#endif
 #ifndef SRS_LOCAL_RANK_SPLIT
 #define SRS_LOCAL_RANK_SPLIT 2
 #endif
@@ -146,12 +149,18 @@ static_assert((kSampleMaxChunks + kSampleWGs - 1) / kSampleWGs * kSampleChunk < 
 constexpr int kLocalItems = SRS_LOCAL_ITEMS;
 constexpr int kLocalThreads = SRS_LOCAL_THREADS;
 constexpr int kLocalCap = kLocalThreads * kLocalItems;    // 8192 keys per segment
-constexpr int kLocalItemsSmall = 8;
-constexpr int kLocalThreadsSmall = 512;
+#ifndef SRS_LOCAL_SMALL_THREADS
+#define SRS_LOCAL_SMALL_THREADS 512
+#endif
+#ifndef SRS_LOCAL_SMALL_WGS_PER_CU
+#define SRS_LOCAL_SMALL_WGS_PER_CU 3
+#endif
+constexpr int kLocalThreadsSmall = SRS_LOCAL_SMALL_THREADS;
+constexpr int kLocalItemsSmall = 4096 / kLocalThreadsSmall;
 constexpr int kLocalCapSmall = kLocalThreadsSmall * kLocalItemsSmall;  // 4096
 // occupancy the LDS footprint allows (90 KB -> 1 block/CU; 49 KB -> 3 blocks/CU)
 constexpr int kLocalWavesPerEU = kLocalThreads / 64 / 4;
-constexpr int kLocalWavesPerEUSmall = 3 * kLocalThreadsSmall / 64 / 4;
+constexpr int kLocalWavesPerEUSmall = SRS_LOCAL_SMALL_WGS_PER_CU * kLocalThreadsSmall / 64 / 4;
 #ifndef SRS_LOCAL_STABLE_ITEMS
 #define SRS_LOCAL_STABLE_ITEMS 8
 #endif

@@ -1023,7 +1023,7 @@ struct ScatterLds {
   uint64_t sval[kTile];
   // digit of each staged slot (LUT passes recompute it instead: their 24 KB
   // table must leave room for two workgroups per CU)
-  uint16_t sdig[LUT ? 1 : kTile];
+  uint16_t sdig[(LUT || !SRS_SCATTER_SDIG) ? 1 : kTile];
   alignas(8) uint16_t wc[kScatterThreads / 64][kMaxBins];  // zeroed as u64
   uint16_t bin_start[kMaxBins];  // tile offsets <= kTile fit 16 bits
   int64_t gdst[kMaxBins];
@@ -1137,7 +1137,7 @@ __device__ __forceinline__ void scatter_process_tile(
       const uint32_t d = dg[k];
       pos[k] = L.bin_start[d] + L.wc[wave][d] + pos[k];
       L.sval[pos[k]] = v0[k];
-      if constexpr (!LUT) L.sdig[pos[k]] = (uint16_t)d;
+      if constexpr (!LUT && SRS_SCATTER_SDIG) L.sdig[pos[k]] = (uint16_t)d;
     }
   }
   lds_barrier();
@@ -1156,10 +1156,14 @@ __device__ __forceinline__ void scatter_process_tile(
         if (j < cnt) {
           const uint64_t x = L.sval[j];
           uint32_t d;
-          if constexpr (LUT) d = pass_digit<LUT>(xf((U)(x & kmask)), P.shift, mask, lut);
+          if constexpr (LUT || !SRS_SCATTER_SDIG) d = pass_digit<LUT>(xf((U)(x & kmask)), P.shift, mask, lut);
           else d = L.sdig[j];
           dout[i] = (uint16_t)d;
+          #ifdef SRS_DIAG_SEQW
+          stw<decltype(W_)::value>(out + ((int64_t)j + ti.base) * (int64_t)st, x);
+#else
           stw<decltype(W_)::value>(out + ((int64_t)j + L.gdst[d]) * (int64_t)st, x);
+#endif
         }
       }
     });
@@ -1191,8 +1195,12 @@ __device__ __forceinline__ void scatter_process_tile(
       for (int i = 0; i < IT; i++) {
         const int j = i * NT + (int)threadIdx.x;
         if (j < cnt)
+          #ifdef SRS_DIAG_SEQW
+          stw<decltype(W_)::value>(out + ((int64_t)j + ti.base) * (int64_t)cst, L.sval[j]);
+#else
           stw<decltype(W_)::value>(out + ((int64_t)j + L.gdst[dout[i]]) * (int64_t)cst,
                                    L.sval[j]);
+#endif
       }
     });
   };
@@ -1408,9 +1416,13 @@ __global__ __launch_bounds__(NT, WPE) void local_kernel(const SortDesc* __restri
       // key value and a STABLE bucket pass (ballot ranks, input order inside
       // a bucket) is the final order. Duplicate-heavy data (C2's floats) lands
       // here; no bucket-size limit. Per-wave counters [NW][nb] live in sbuf.
+      constexpr bool kWcFits = NW * NB * sizeof(uint16_t) <= CAP * sizeof(uint64_t);
+      if constexpr (!kWcFits) {  // (tuning shapes only) the stable kernel takes it
+        if (threadIdx.x == 0) fallback[atomicAdd(fallback_count, 1ull)] = g;
+        return;
+      }
       uint16_t* wc = (uint16_t*)sbuf;
-      static_assert(NW * NB * sizeof(uint16_t) <= CAP * sizeof(uint64_t), "wc fits sbuf");
-      const uint32_t nb = 1u << nbits;
+      const uint32_t nb = kWcFits ? 1u << nbits : 1u;
       for (uint32_t i = threadIdx.x; i < NW * nb / 2; i += NT) ((uint32_t*)wc)[i] = 0;
       auto digit = [&](int k) -> uint32_t { return (uint32_t)(ukey(k) >> lo) & mask; };
       lds_barrier();

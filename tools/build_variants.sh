@@ -9,7 +9,7 @@ for spec in "$@"; do
   pids=()
   for f in srs_kernels srs_api; do
     /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -munsafe-fp-atomics $flags \
-      -c csrc/$f.hip -o build/v_$name/$f.o &
+      -Rpass-analysis=kernel-resource-usage -c csrc/$f.hip -o build/v_$name/$f.o 2> build/v_$name/$f.remarks &
     pids+=($!)
   done
   for p in "${pids[@]}"; do wait $p || { echo "FAILED $name"; exit 1; }; done

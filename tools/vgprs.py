@@ -1,10 +1,10 @@
 """Print VGPRs / scratch / occupancy per kernel from the build's remarks.
-usage: python tools/vgprs.py [substring]"""
+usage: python tools/vgprs.py [substring] [remarks file]"""
 import re
 import sys
 
 pat = sys.argv[1] if len(sys.argv) > 1 else ""
-txt = open("simd-radix-sort_amd/build/srs_kernels.remarks").read()
+txt = open(sys.argv[2] if len(sys.argv) > 2 else "simd-radix-sort_amd/build/srs_kernels.remarks").read()
 cur, row = None, {}
 for line in txt.splitlines():
     m = re.search(r"Function Name: (\S+)", line)
