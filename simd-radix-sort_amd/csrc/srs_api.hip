@@ -894,6 +894,21 @@ int build_soa(Request& R, int64_t num, int kind, int up, int64_t thresh, void* k
   return SRS_OK;
 }
 
+// Device columns are read and written as whole 1/2/4/8-byte words, so every
+// device pointer must be aligned to its word (hipMalloc and torch
+// allocations always are). Host arrays may be unaligned, as in the reference
+// (loadu, src/simd.hpp): they are staged through HBM.
+int check_device_alignment(const Request& R) {
+  if (R.num <= 1) return SRS_OK;
+  for (int c = 0; c < R.ncols; c++) {
+    const uint32_t a = R.aos ? (R.elem_size < 8 ? R.elem_size : 8) : R.widths[c];
+    if (((uintptr_t)R.in_cols[c] | (uintptr_t)R.out_cols[c]) % a != 0)
+      return fail(SRS_ERR_INVALID_ARG, "device arrays must be aligned to their element size "
+                                       "(records: to min(elem_size, 8))");
+  }
+  return SRS_OK;
+}
+
 int build_aos(Request& R, int64_t num, int kind, int up, int64_t thresh, void* elems,
               uint32_t esz, void* elems_out) {
   SRS_TRY(validate_common(num, kind));
@@ -946,6 +961,7 @@ int srs_sort_soa_device(int64_t num, int key_kind, int up, int64_t cmp_sort_thre
   Request R;
   SRS_TRY(build_soa(R, num, key_kind, up, cmp_sort_threshold, keys, num_payloads, payloads,
                     payload_sizes, keys_out, payloads_out));
+  SRS_TRY(check_device_alignment(R));
   return sort_device(R, (hipStream_t)stream);
 }
 
@@ -965,6 +981,7 @@ int srs_sort_segments_device(int64_t num, int key_kind, int up, void* keys,
   Request R;
   SRS_TRY(build_soa(R, num, key_kind, up, 0, keys, num_payloads, payloads, payload_sizes,
                     nullptr, nullptr));
+  SRS_TRY(check_device_alignment(R));
   if (num_segments == 0 || num <= 1) return SRS_OK;
   R.seg_bounds = segment_bounds;
   R.nsegs = num_segments;
@@ -983,6 +1000,7 @@ int srs_sort_aos_device(int64_t num, int key_kind, int up, int64_t cmp_sort_thre
   Request R;
   SRS_TRY(build_aos(R, num, key_kind, up, cmp_sort_threshold, elements, elem_size,
                     elements_out));
+  SRS_TRY(check_device_alignment(R));
   return sort_device(R, (hipStream_t)stream);
 }
 
@@ -1023,6 +1041,8 @@ int srs_key_histogram_device(int64_t num, int key_kind, int up, const void* keys
     return fail(SRS_ERR_INVALID_ARG, "bits must be in [1, min(12, key bits)]");
   if (num <= 0) return SRS_OK;
   if (!keys || !hist) return fail(SRS_ERR_INVALID_ARG, "NULL pointer");
+  if ((uintptr_t)keys % ks != 0 || (uintptr_t)hist % 8 != 0)
+    return fail(SRS_ERR_INVALID_ARG, "device arrays must be aligned to their element size");
   SortDesc d;
   memset(&d, 0, sizeof d);
   key_masks(key_kind, up, d);
@@ -1049,6 +1069,7 @@ int srs_partition_device(int64_t num, int key_kind, int up, const void* keys,
   SRS_TRY(build_soa(R, num, key_kind, up, 0, (void*)keys, num_payloads, (void* const*)payloads,
                     payload_sizes, keys_out, payloads_out));
   if (!keys_out) return fail(SRS_ERR_INVALID_ARG, "keys_out is NULL");
+  SRS_TRY(check_device_alignment(R));
   if (num == 1) {
     // a single key: its group from the table, then a plain copy
     int32_t one = 0;

@@ -67,6 +67,22 @@ def test_argument_validation_without_gpu():
     assert lib.srs_sort_soa(1, 4, 1, 16, k.ctypes.data, 0, None, None) == 0
     assert lib.srs_sort_soa(-5, 4, 1, 16, k.ctypes.data, 0, None, None) == 0
     assert srs_amd.version().startswith("srs_amd")
+    # device arrays must be word-aligned (rejected before any device access;
+    # the addresses below are never dereferenced)
+    fn = lib.srs_sort_soa_device
+    fn.argtypes = [ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int64, ctypes.c_void_p,
+                   ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                   ctypes.c_void_p, ctypes.c_void_p]
+    assert fn(4, 6, 1, 16, 0x10004, 0, None, None, None, None, None) == -1  # u64 at +4
+    assert b"aligned" in lib.srs_last_error()
+    p8 = (ctypes.c_void_p * 1)(0x20002)
+    s8 = (ctypes.c_uint32 * 1)(8)
+    assert fn(4, 4, 1, 16, 0x10000, 1, p8, s8, None, None, None) == -1  # u64 payload at +2
+    fa = lib.srs_sort_aos_device
+    fa.argtypes = [ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int64, ctypes.c_void_p,
+                   ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]
+    assert fa(4, 4, 1, 16, 0x10004, 16, None, None) == -1  # 16-byte records at +4
+    assert b"aligned" in lib.srs_last_error()
 
 
 def _kernel_resources():

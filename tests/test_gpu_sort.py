@@ -156,6 +156,32 @@ def test_distributions_vs_stable_and_oracle(kind, up):
                 assert bytes_equal(k, ok) and bytes_equal(a, op), (dist, n, "oracle")
 
 
+def test_unaligned_host_arrays():
+    """The reference takes unaligned arrays (loadu, src/simd.hpp); the host
+    drop-in stages them through HBM, so byte-offset views sort like aligned
+    ones. (Device arrays must be word-aligned: test_capi checks the error.)"""
+    n = 100003
+    keys = make_keys(6, "uniform", n, 7)
+    pay = payload_of(keys, 4)
+    kb = np.zeros(n * 8 + 3, np.uint8)
+    pb = np.zeros(n * 4 + 1, np.uint8)
+    k = kb[3:].view(np.uint64)
+    p = pb[1:].view(np.uint32)
+    assert k.ctypes.data % 8 and p.ctypes.data % 4
+    k[:] = keys
+    p[:] = pay
+    srs_amd.sort(k, p)
+    ok, op = keys.copy(), pay.copy()
+    oracle_sort_soa(6, True, ok, [op])
+    assert bytes_equal(k, ok) and bytes_equal(p, op)
+    rec = np.zeros(n * 16 + 1, np.uint8)[1:].reshape(n, 16)
+    rec[:, :8] = keys.view(np.uint8).reshape(n, 8)
+    rec[:, 8:] = payload_of(keys, 8).view(np.uint8).reshape(n, 8)
+    want = stable_aos(6, True, rec.copy())
+    srs_amd.sort_combined(rec, 6)
+    assert bytes_equal(rec, want)
+
+
 @pytest.mark.parametrize("n", [0, 1, 2, 3, 15, 16, 17, 63, 64, 65, 4095, 4096, 8191, 8192,
                                8193, 12287, 16384, 16385, 24577, 100003, 1 << 20])
 def test_sizes_u64_vs_oracle(n):
