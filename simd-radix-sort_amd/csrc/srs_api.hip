@@ -206,6 +206,10 @@ struct Workspace {
   // before its first workspace write (WsUse).
   hipEvent_t idle = nullptr;
   bool idle_pending = false;
+  // single-launch small sorts (run_small): which fallback bodies ran, for
+  // srs_debug_last_fallbacks
+  DevBuf small_taken;
+  bool last_small = false;
 };
 
 std::mutex g_wmu;
@@ -511,11 +515,82 @@ int run_level(Workspace* W, int ks, const SortDesc* d_desc, LevelState& S, int f
   return SRS_OK;
 }
 
-int run_sort(Workspace* W, const Request& R, hipStream_t st) {
+// Descriptor columns of a request: IN / OUT are the caller's arrays, TMP /
+// TMP2 the workspace (AoS records as one column, or as 8-byte slices that are
+// dense SoA columns in the workspace when aos_cols).
+void set_columns(const Request& R, SortDesc& d, char* tmp, char* tmp2, bool aos_cols,
+                 size_t slice_bytes, const size_t* tmp_off, bool inplace) {
   const int ks = key_size_of(R.kind);
-  const int64_t n = R.num;
+  if (R.aos) {
+    const uint32_t E = R.elem_size;
+    char* in = (char*)R.in_cols[0];
+    char* out = (char*)R.out_cols[0];
+    const uint32_t slice = E < 8 ? E : 8;
+    int nc = 0;
+    for (uint32_t off = 0; off < E; off += slice, nc++) {
+      if (aos_cols)  // slice nc: a dense 8-byte column in TMP / TMP2
+        d.cols[nc] = Col{{in + off, out + off, tmp + nc * slice_bytes, tmp2 + nc * slice_bytes},
+                         slice, {E, E, 8, 8}};
+      else
+        d.cols[nc] = Col{{in + off, out + off, tmp ? tmp + off : nullptr, nullptr}, slice,
+                         {E, E, E, E}};
+    }
+    d.ncols = nc;
+    d.key = d.cols[0];
+    d.key.width = (uint32_t)ks;  // the key: low bytes of slice 0
+  } else {
+    for (int c = 0; c < R.ncols; c++) {
+      const uint32_t w = R.widths[c];
+      d.cols[c] = Col{{(char*)R.in_cols[c], (char*)R.out_cols[c], tmp ? tmp + tmp_off[c] : nullptr,
+                       nullptr}, w, {w, w, w, w}};
+    }
+    d.key = d.cols[0];
+    d.ncols = R.ncols;
+  }
+  if (inplace)  // IN aliases OUT: a segment that never moved is already home
+    for (int c = 0; c < d.ncols; c++) d.cols[c].base[BUF_IN] = d.cols[c].base[BUF_OUT];
+}
+
+bool is_inplace(const Request& R) {
   bool inplace = true;
   for (int c = 0; c < R.ncols; c++) inplace &= (R.in_cols[c] == R.out_cols[c]);
+  return inplace;
+}
+
+// n <= kLocalCap (and no segment list): the whole sort is one local segment,
+// sorted by one single-workgroup launch that takes the descriptor as a kernel
+// argument. No workspace memory is touched (the input and output arrays
+// only), so no stream-order wait on the workspace either.
+int run_small(Workspace* W, const Request& R, hipStream_t st) {
+  const int ks = key_size_of(R.kind);
+  const int64_t n = R.num;
+  const bool inplace = is_inplace(R);
+  SortDesc d;
+  memset(&d, 0, sizeof d);
+  key_masks(R.kind, R.up, d);
+  const bool is_float = R.kind == SRS_KEY_F32 || R.kind == SRS_KEY_F64;
+  d.canon_zero = (is_float && n <= R.thresh) ? 1 : 0;
+  const int ksl = ks | (d.canon_zero ? SRS_KS_CANON : 0);
+  set_columns(R, d, nullptr, nullptr, false, 0, nullptr, inplace);
+  d.stamp_acc = g_stamp_acc;
+  const Seg g{0, n, d.key_bits, inplace ? BUF_OUT : BUF_IN};
+  SRS_TRY(ensure(W->small_taken, 2 * sizeof(int64_t)));
+  W->last_small = true;
+  note_elems("local", (double)n);
+  {
+    TimedScope ts("local", (double)0, st);
+    launch_small_sort(ksl, d, g, (int64_t*)W->small_taken.p, st);
+  }
+  HIP_TRY(hipGetLastError());
+  return SRS_OK;
+}
+
+int run_sort(Workspace* W, const Request& R, hipStream_t st) {
+  if (R.nsegs == 0 && R.num <= kLocalCap) return run_small(W, R, st);
+  W->last_small = false;
+  const int ks = key_size_of(R.kind);
+  const int64_t n = R.num;
+  const bool inplace = is_inplace(R);
 
   // ---- descriptor: key view + columns (AoS records as <= 8-byte slices) --
   SortDesc d;
@@ -551,33 +626,7 @@ int run_sort(Workspace* W, const Request& R, hipStream_t st) {
     d.tmp2 = 1;
   }
 
-  if (R.aos) {
-    const uint32_t E = R.elem_size;
-    char* in = (char*)R.in_cols[0];
-    char* out = (char*)R.out_cols[0];
-    const uint32_t slice = E < 8 ? E : 8;
-    int nc = 0;
-    for (uint32_t off = 0; off < E; off += slice, nc++) {
-      if (aos_cols)  // slice nc: a dense 8-byte column in TMP / TMP2
-        d.cols[nc] = Col{{in + off, out + off, tmp + nc * slice_bytes, tmp2 + nc * slice_bytes},
-                         slice, {E, E, 8, 8}};
-      else
-        d.cols[nc] = Col{{in + off, out + off, tmp + off, nullptr}, slice, {E, E, E, E}};
-    }
-    d.ncols = nc;
-    d.key = d.cols[0];
-    d.key.width = (uint32_t)ks;  // the key: low bytes of slice 0
-  } else {
-    for (int c = 0; c < R.ncols; c++) {
-      const uint32_t w = R.widths[c];
-      d.cols[c] = Col{{(char*)R.in_cols[c], (char*)R.out_cols[c], tmp + tmp_off[c], nullptr}, w,
-                      {w, w, w, w}};
-    }
-    d.key = d.cols[0];
-    d.ncols = R.ncols;
-  }
-  if (inplace)  // IN aliases OUT: a segment that never moved is already home
-    for (int c = 0; c < d.ncols; c++) d.cols[c].base[BUF_IN] = d.cols[c].base[BUF_OUT];
+  set_columns(R, d, tmp, tmp2, aos_cols, slice_bytes, tmp_off.data(), inplace);
 
   d.stamp_acc = g_stamp_acc;
   bool balanced = false;
@@ -821,6 +870,7 @@ int sort_device(Request& R, hipStream_t st) {
   std::lock_guard<std::mutex> lk(g_wmu);
   Workspace* W = nullptr;
   SRS_TRY(get_ws(&W));
+  if (R.num <= kLocalCap) return run_small(W, R, st);  // touches no workspace data
   WsUse use;
   SRS_TRY(use.begin(W, st));
   return run_sort(W, R, st);
@@ -1132,6 +1182,11 @@ int srs_debug_last_fallbacks(int64_t* counts) {
   Workspace* W = nullptr;
   SRS_TRY(get_ws(&W));
   counts[0] = counts[1] = 0;
+  if (W->last_small) {
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpy(counts, W->small_taken.p, 2 * sizeof(int64_t), hipMemcpyDeviceToHost));
+    return SRS_OK;
+  }
   if (!W->ctr.p) return SRS_OK;
   HIP_TRY(hipDeviceSynchronize());
   ListCounters c;
@@ -1152,7 +1207,7 @@ int srs_release_workspace(void) {
     DevBuf* bufs[] = {&w->tmp, &w->tmp2, &w->stage, &w->desc, &w->big[0], &w->big[1], &w->local, &w->local2, &w->fallback, &w->fallback2, &w->shist, &w->lut, &w->lut_rbits,
                       &w->copy, &w->plan, &w->tcount, &w->gcount, &w->tbase, &w->gbase,
                       &w->var, &w->sbase, &w->tile_seg, &w->group_seg, &w->hist, &w->offs,
-                      &w->gsum, &w->gofs, &w->scan_tmp, &w->totals, &w->ctr};
+                      &w->gsum, &w->gofs, &w->scan_tmp, &w->totals, &w->ctr, &w->small_taken};
     for (DevBuf* b : bufs)
       if (b->p) (void)hipFree(b->p);
     (void)hipHostFree(w->h_ctr);

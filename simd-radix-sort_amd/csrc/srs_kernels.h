@@ -44,6 +44,8 @@ void launch_local(int key_size, const SortDesc* d, const Seg* segs, int64_t nseg
 void launch_local_stable(int key_size, const SortDesc* d, const Seg* segs,
                          const unsigned long long* nsegs, int big_class, Seg* fallback,
                          unsigned long long* fallback_count, int grid, hipStream_t st);
+// n <= kLocalCap: the whole sort in one single-workgroup launch
+void launch_small_sort(int key_size, const SortDesc& d, Seg g, int64_t* taken, hipStream_t st);
 void launch_local_lsd(int key_size, const SortDesc* d, const Seg* segs,
                       const unsigned long long* nsegs, int grid, hipStream_t st);
 int64_t sample_partial_bytes();

@@ -1321,11 +1321,25 @@ __device__ __forceinline__ void local_digit_pass(
 // Fast path: bucket pass with LDS atomics (order inside a bucket arbitrary);
 // the rank step then restores the stable order from the packed
 // (key bits, original index) words.
-template <typename KT, typename U, int NT, int IT, int WPE, bool CZ>
-__global__ __launch_bounds__(NT, WPE) void local_kernel(const SortDesc* __restrict__ desc,
-                                                   const Seg* __restrict__ segs,
-                                                   Seg* __restrict__ fallback,
-                                                   unsigned long long* fallback_count) {
+template <int NT, int IT>
+struct FastLds {
+  // sbuf: packed sort words (+ rank sentinels) during the sort, column
+  // staging afterwards
+  uint64_t sbuf[NT * IT + kRankSortMax];
+  uint16_t perm[NT * IT];                      // output slot -> original index
+  uint32_t hist2[(1 << kLocalTopBits) / 2];    // 16-bit bucket sizes, then cursors (pairs)
+  uint16_t bin_start[(1 << kLocalTopBits) + 2];
+  uint32_t scan_sh[NT / 64 + 1];
+  unsigned long long sh_or;
+  int maxlen;
+};
+
+// One segment g (<= NT * IT records) by one workgroup. Returns true when the
+// segment goes to the stable path instead (nothing written to global memory
+// then); block-uniform.
+template <typename KT, typename U, int NT, int IT, bool CZ>
+__device__ __forceinline__ bool local_fast_body(const SortDesc* __restrict__ desc, const Seg g,
+                                                FastLds<NT, IT>& Ls) {
   constexpr int NW = NT / 64;
   constexpr int CAP = NT * IT;
   constexpr int IDXB = CAP <= 4096 ? 12 : 13;  // bits of an index inside the segment
@@ -1334,17 +1348,13 @@ __global__ __launch_bounds__(NT, WPE) void local_kernel(const SortDesc* __restri
   constexpr int BPT = NB / NT;  // bins per thread (an even count: packed pairs)
   static_assert(BPT * NT == NB && BPT % 2 == 0, "bins per thread");
   static_assert(CAP < 65536, "16-bit bucket counters");
-  // sbuf: packed sort words (+ rank sentinels) during the sort, column
-  // staging afterwards
-  __shared__ uint64_t sbuf[CAP + kRankSortMax];
-  __shared__ uint16_t perm[CAP];          // output slot -> original index
-  __shared__ uint32_t hist2[NB / 2];      // 16-bit bucket sizes, then cursors (pairs)
-  __shared__ uint16_t bin_start[NB + 2];
-  __shared__ uint32_t scan_sh[NW + 1];
-  __shared__ unsigned long long sh_or;
-  __shared__ int maxlen;
-
-  const Seg g = segs[blockIdx.x];
+  auto& sbuf = Ls.sbuf;
+  auto& perm = Ls.perm;
+  auto& hist2 = Ls.hist2;
+  auto& bin_start = Ls.bin_start;
+  auto& scan_sh = Ls.scan_sh;
+  auto& sh_or = Ls.sh_or;
+  auto& maxlen = Ls.maxlen;
   const uint32_t wave = threadIdx.x >> 6;
   const uint32_t lane = lane_id();
   const int ebase = (int)wave * IT * 64 + (int)lane;  // element of slot k: ebase + 64 k
@@ -1405,8 +1415,7 @@ __global__ __launch_bounds__(NT, WPE) void local_kernel(const SortDesc* __restri
     // to the stable kernel.
     const bool wide = !exact && hi + 1 + IDXB > 64;
     if (wide && sh - lo + IDXB > 64) {
-      if (threadIdx.x == 0) fallback[atomicAdd(fallback_count, 1ull)] = g;
-      return;
+      return true;  // the stable kernel takes it
     }
     const uint64_t below = (sh - lo >= 64) ? ~0ull : ((1ull << (sh - lo)) - 1);
     const uint32_t mask = (1u << nbits) - 1;
@@ -1418,8 +1427,7 @@ __global__ __launch_bounds__(NT, WPE) void local_kernel(const SortDesc* __restri
       // here; no bucket-size limit. Per-wave counters [NW][nb] live in sbuf.
       constexpr bool kWcFits = NW * NB * sizeof(uint16_t) <= CAP * sizeof(uint64_t);
       if constexpr (!kWcFits) {  // (tuning shapes only) the stable kernel takes it
-        if (threadIdx.x == 0) fallback[atomicAdd(fallback_count, 1ull)] = g;
-        return;
+        return true;
       }
       uint16_t* wc = (uint16_t*)sbuf;
       const uint32_t nb = kWcFits ? 1u << nbits : 1u;
@@ -1520,7 +1528,6 @@ __global__ __launch_bounds__(NT, WPE) void local_kernel(const SortDesc* __restri
     if (maxlen > kRankSortMax) {
       // a large bucket (duplicates or skew): local_stable_kernel takes the
       // segment (nothing has been written to global memory yet)
-      if (threadIdx.x == 0) fallback[atomicAdd(fallback_count, 1ull)] = g;
       return true;
     }
 #pragma unroll
@@ -1633,7 +1640,7 @@ __global__ __launch_bounds__(NT, WPE) void local_kernel(const SortDesc* __restri
     return false;
     };  // bucket_rank
     if (direct) {
-      if (bucket_rank(std::true_type{})) return;
+      if (bucket_rank(std::true_type{})) return true;
       // ---- 4'. column 0 from the words; the rank left each output slot's
       // word slot in perm. u = known top bits | word bits, then the inverse
       // key transform. The other columns staged, written in order. FW: the
@@ -1687,12 +1694,12 @@ __global__ __launch_bounds__(NT, WPE) void local_kernel(const SortDesc* __restri
       else direct_out(std::integral_constant<int, 0>{});
       STAMP();  // 6
       STAMP_FLUSH(1);
-      return;
+      return false;
     }
-    if (bucket_rank(std::false_type{})) return;
+    if (bucket_rank(std::false_type{})) return true;
     }  // atomic bucket pass + rank
   } else if (g.buf == BUF_OUT) {
-    return;  // all keys equal and already home
+    return false;  // all keys equal and already home
   } else {
 #pragma unroll
     for (int k = 0; k < IT; k++) perm[ebase + k * 64] = (uint16_t)(ebase + k * 64);
@@ -1734,17 +1741,45 @@ __global__ __launch_bounds__(NT, WPE) void local_kernel(const SortDesc* __restri
   }
   STAMP();  // 6: columns moved
   STAMP_FLUSH(1);
+  return false;
+}
+
+template <typename KT, typename U, int NT, int IT, int WPE, bool CZ>
+__global__ __launch_bounds__(NT, WPE) void local_kernel(const SortDesc* __restrict__ desc,
+                                                   const Seg* __restrict__ segs,
+                                                   Seg* __restrict__ fallback,
+                                                   unsigned long long* fallback_count) {
+  __shared__ FastLds<NT, IT> Ls;
+  const Seg g = segs[blockIdx.x];
+  if (local_fast_body<KT, U, NT, IT, CZ>(desc, g, Ls) && threadIdx.x == 0)
+    fallback[atomicAdd(fallback_count, 1ull)] = g;
 }
 
 // Stable path for segments the fast kernel handed over (a top-digit bucket
 // larger than kRankSortMax): the bucket pass ranks with ballots (stable), so
 // buckets whose keys are all equal are final; only mixed buckets are ranked.
 // Grid-stride over a device-side list whose length is read on device.
+template <int NT>
+struct StableLds {
+  static constexpr int CAP = NT * kLocalStableItems;
+  static constexpr int NB = 1 << kLocalStableTopBits;
+  static constexpr int WCP = (NT / 64) * NB > CAP ? (NT / 64) * NB : CAP;
+  // sbuf: packed sort words during the sort, column staging afterwards
+  uint64_t sbuf[CAP];
+  uint16_t wc_perm[WCP];       // ballot counters [NW][NB], then perm[CAP]
+  uint32_t bflag[NB];          // bucket holds differing keys
+  uint16_t sorig[CAP];         // wide words: original index by slot
+  uint32_t bin_start[NB + 1];
+  uint32_t scan_sh[NT / 64 + 1];
+  unsigned long long sh_or;
+  int maxlen;
+};
+
+// One segment g by one workgroup; true: the segment goes on to the LSD path
+// (nothing written to global memory then). Block-uniform.
 template <typename KT, typename U, int NT, bool CZ>
-__global__ __launch_bounds__(NT) void local_stable_kernel(
-    const SortDesc* __restrict__ desc, const Seg* __restrict__ segs,
-    const unsigned long long* __restrict__ nsegs, Seg* __restrict__ fallback,
-    unsigned long long* fallback_count) {
+__device__ __forceinline__ bool local_stable_body(const SortDesc* __restrict__ desc, const Seg g,
+                                                  StableLds<NT>& Ls) {
   constexpr int IT = kLocalStableItems;
   constexpr int NW = NT / 64;
   constexpr int CAP = NT * IT;
@@ -1753,16 +1788,15 @@ __global__ __launch_bounds__(NT) void local_stable_kernel(
   constexpr int NB = 1 << kLocalStableTopBits;
   constexpr int BPT = NB >= NT ? NB / NT : 1;  // bins per thread (threads >= NB idle)
   static_assert(BPT * NT >= NB, "bins per thread");
-  constexpr int WCP = NW * NB > CAP ? NW * NB : CAP;
-  // sbuf: packed sort words during the sort, column staging afterwards
-  __shared__ uint64_t sbuf[CAP];
-  __shared__ uint16_t wc_perm[WCP];       // ballot counters [NW][NB], then perm[CAP]
-  __shared__ uint32_t bflag[NB];          // bucket holds differing keys
-  __shared__ uint16_t sorig[CAP];         // wide words: original index by slot
-  __shared__ uint32_t bin_start[NB + 1];
-  __shared__ uint32_t scan_sh[NW + 1];
-  __shared__ unsigned long long sh_or;
-  __shared__ int maxlen;
+  constexpr int WCP = StableLds<NT>::WCP;
+  auto& sbuf = Ls.sbuf;
+  auto& wc_perm = Ls.wc_perm;
+  auto& bflag = Ls.bflag;
+  auto& sorig = Ls.sorig;
+  auto& bin_start = Ls.bin_start;
+  auto& scan_sh = Ls.scan_sh;
+  auto& sh_or = Ls.sh_or;
+  auto& maxlen = Ls.maxlen;
   uint16_t* perm = wc_perm;               // output slot -> original index
 
   const uint32_t wave = threadIdx.x >> 6;
@@ -1773,9 +1807,6 @@ __global__ __launch_bounds__(NT) void local_stable_kernel(
   const int ncols = desc->ncols;
   const int kbytes = desc->key_bits >> 3;
   const uint64_t kmask = kbytes == 8 ? ~0ull : ((1ull << (8 * kbytes)) - 1);
-  const unsigned long long total = *nsegs;
-  for (unsigned long long si = blockIdx.x; si < total; si += gridDim.x) {
-  const Seg g = segs[si];
   const int cnt = (int)g.len;
   const int64_t base = g.start;
   __syncthreads();  // the previous segment is done with the shared arrays
@@ -1908,8 +1939,7 @@ with_width(w, [&](auto W_) {
     if (maxlen > kRankSortMax) {
       // a large bucket of differing keys: local_lsd_kernel takes the segment
       // (nothing has been written to global memory yet)
-      if (threadIdx.x == 0) fallback[atomicAdd(fallback_count, 1ull)] = g;
-      continue;
+      return true;
     }
     // ---- 4. rank inside mixed buckets: #(words of the bucket below mine) --
     // The word orders by (key, original index): stable. Slots in two halves
@@ -1971,7 +2001,7 @@ with_width(w, [&](auto W_) {
     lds_barrier();
     }  // !exact
   } else if (g.buf == BUF_OUT) {
-    continue;  // all keys equal and already home
+    return false;  // all keys equal and already home
   } else {
 #pragma unroll
     for (int k = 0; k < IT; k++) perm[ebase + k * 64] = (uint16_t)(ebase + k * 64);
@@ -2016,6 +2046,20 @@ with_width(w, [&](auto W_) {
       }
     });
   }
+  return false;
+}
+
+template <typename KT, typename U, int NT, bool CZ>
+__global__ __launch_bounds__(NT) void local_stable_kernel(
+    const SortDesc* __restrict__ desc, const Seg* __restrict__ segs,
+    const unsigned long long* __restrict__ nsegs, Seg* __restrict__ fallback,
+    unsigned long long* fallback_count) {
+  __shared__ StableLds<NT> Ls;
+  const unsigned long long total = *nsegs;
+  for (unsigned long long si = blockIdx.x; si < total; si += gridDim.x) {
+    const Seg g = segs[si];
+    if (local_stable_body<KT, U, NT, CZ>(desc, g, Ls) && threadIdx.x == 0)
+      fallback[atomicAdd(fallback_count, 1ull)] = g;
   }
 }
 
@@ -2023,21 +2067,28 @@ with_width(w, [&](auto W_) {
 // Fallback for segments whose top-digit buckets are too large for the rank
 // step (skewed keys): stable LSD passes (ballot ranks) over every varying
 // bit. Grid-stride over a device-side list whose length is read on device.
+struct LsdLds {
+  static constexpr int CAP = kLocalStableThreads * kLocalStableItems;
+  uint64_t sbuf[CAP];
+  uint16_t sidx[CAP];
+  uint16_t wc[kLocalStableThreads / 64][1 << kLocalBits];
+  uint32_t bin_start[(1 << kLocalBits) + 1];
+  uint32_t scan_sh[kLocalStableThreads / 64 + 1];
+  unsigned long long sh_or;
+};
+
+// One segment g by one workgroup of kLocalStableThreads (always finishes it).
 template <typename KT, typename U, bool CZ>
-__global__ __launch_bounds__(kLocalStableThreads) void local_lsd_kernel(
-    const SortDesc* __restrict__ desc, const Seg* __restrict__ segs,
-    const unsigned long long* __restrict__ nsegs) {
+__device__ __forceinline__ void local_lsd_body(const SortDesc* __restrict__ desc, const Seg g,
+                                               LsdLds& Ls) {
   constexpr int NT = kLocalStableThreads;
   constexpr int IT = kLocalStableItems;
-  constexpr int NW = NT / 64;
-  constexpr int CAP = NT * IT;
-  constexpr int NB = 1 << kLocalBits;
-  __shared__ uint64_t sbuf[CAP];
-  __shared__ uint16_t sidx[CAP];
-  __shared__ uint16_t wc[NW][NB];
-  __shared__ uint32_t bin_start[NB + 1];
-  __shared__ uint32_t scan_sh[NW + 1];
-  __shared__ unsigned long long sh_or;
+  auto& sbuf = Ls.sbuf;
+  auto& sidx = Ls.sidx;
+  auto& wc = Ls.wc;
+  auto& bin_start = Ls.bin_start;
+  auto& scan_sh = Ls.scan_sh;
+  auto& sh_or = Ls.sh_or;
   U* su = (U*)sbuf;
   const uint32_t wave = threadIdx.x >> 6;
   const int ebase = (int)wave * IT * 64 + (int)lane_id();
@@ -2046,9 +2097,7 @@ __global__ __launch_bounds__(kLocalStableThreads) void local_lsd_kernel(
   const int ncols = desc->ncols;
   const int kbytes = desc->key_bits >> 3;
   const uint64_t kmask = kbytes == 8 ? ~0ull : ((1ull << (8 * kbytes)) - 1);
-  const unsigned long long total = *nsegs;
-  for (unsigned long long si = blockIdx.x; si < total; si += gridDim.x) {
-    const Seg g = segs[si];
+  {
     const int cnt = (int)g.len;
     const int64_t base = g.start;
     __syncthreads();
@@ -2119,6 +2168,52 @@ __global__ __launch_bounds__(kLocalStableThreads) void local_lsd_kernel(
         }
       });
     }
+  }
+}
+
+template <typename KT, typename U, bool CZ>
+__global__ __launch_bounds__(kLocalStableThreads) void local_lsd_kernel(
+    const SortDesc* __restrict__ desc, const Seg* __restrict__ segs,
+    const unsigned long long* __restrict__ nsegs) {
+  __shared__ LsdLds Ls;
+  const unsigned long long total = *nsegs;
+  for (unsigned long long si = blockIdx.x; si < total; si += gridDim.x)
+    local_lsd_body<KT, U, CZ>(desc, segs[si], Ls);
+}
+
+// ---------------------------------------------------------------------------
+// small sorts: n <= kLocalCap in ONE launch
+// ---------------------------------------------------------------------------
+// The whole input is one local segment. Instead of start kernel + segment
+// list + fast / stable / LSD launches (four launches, ~40 us per call), one
+// workgroup runs the three bodies in turn over a union of their LDS, with
+// the descriptor as a kernel argument. taken[0] / taken[1] record whether the
+// stable / LSD body ran (srs_debug_last_fallbacks).
+static_assert(kLocalStableThreads == kLocalThreads, "the three bodies share one workgroup");
+union SmallLds {
+  FastLds<kLocalThreads, kLocalItems> fast;
+  StableLds<kLocalStableThreads> stable;
+  LsdLds lsd;
+};
+
+template <typename KT, typename U, bool CZ>
+__global__ __launch_bounds__(kLocalThreads) void small_sort_kernel(const SortDesc d, const Seg g,
+                                                                   int64_t* taken) {
+  __shared__ SmallLds Ls;
+  const SortDesc* desc = &d;
+  int path = 0;
+  if (local_fast_body<KT, U, kLocalThreads, kLocalItems, CZ>(desc, g, Ls.fast)) {
+    __syncthreads();  // the fast body's LDS is reused
+    path = 1;
+    if (local_stable_body<KT, U, kLocalStableThreads, CZ>(desc, g, Ls.stable)) {
+      __syncthreads();
+      path = 2;
+      local_lsd_body<KT, U, CZ>(desc, g, Ls.lsd);
+    }
+  }
+  if (threadIdx.x == 0 && taken) {
+    taken[0] = path >= 1;
+    taken[1] = path >= 2;
   }
 }
 
@@ -2356,6 +2451,13 @@ void launch_local_lsd(int key_size, const SortDesc* d, const Seg* segs,
                       const unsigned long long* nsegs, int grid, hipStream_t st) {
 #define CALL(KT, U, CZ) \
   local_lsd_kernel<KT, U, CZ><<<(unsigned)grid, kLocalStableThreads, 0, st>>>(d, segs, nsegs)
+  SRS_KEY_DISPATCH(key_size, CALL)
+#undef CALL
+}
+
+void launch_small_sort(int key_size, const SortDesc& d, Seg g, int64_t* taken, hipStream_t st) {
+#define CALL(KT, U, CZ) \
+  small_sort_kernel<KT, U, CZ><<<1, kLocalThreads, 0, st>>>(d, g, taken)
   SRS_KEY_DISPATCH(key_size, CALL)
 #undef CALL
 }
