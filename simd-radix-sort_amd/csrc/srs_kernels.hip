@@ -703,10 +703,41 @@ __global__ __launch_bounds__(kCountThreads) void count_kernel(
   const int cnt = rem < kTile ? (int)rem : kTile;
   const U uref = xf((U)gld<KT>(kp + P.start * (int64_t)ks));
   U raw[kCountItems];
+  // element of item k: a dense 4/8-byte key column is read in 16-byte pieces
+  // (range-checked buffer loads; piece j of thread i holds elements
+  // (j * NT + i) * PER ...), anything else (1/2-byte keys, AoS records)
+  // one key per load. The histogram does not depend on the mapping.
+  constexpr int KB = (int)sizeof(KT);
+  constexpr int PER = KB >= 4 ? 16 / KB : 1;
+  static_assert(kCountItems % PER == 0, "whole 16-byte pieces per thread");
+  const bool vec = KB >= 4 && ks == (uint32_t)KB;
+  auto elem = [&](int k) -> int {
+    return vec ? ((k / PER) * kCountThreads + (int)threadIdx.x) * PER + k % PER
+               : k * kCountThreads + (int)threadIdx.x;
+  };
+  if (vec) {
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    const __amdgpu_buffer_rsrc_t r =
+        strip_rsrc(kp + base * (int64_t)KB, cnt > 0 ? (uint32_t)cnt * KB : 0u);
+    u32x4 c[kCountItems / PER];
 #pragma unroll
-  for (int k = 0; k < kCountItems; k++) {
-    const int e = k * kCountThreads + threadIdx.x;
-    raw[k] = e < cnt ? (U)gld<KT>(kp + (base + e) * (int64_t)ks) : (U)0;
+    for (int j = 0; j < kCountItems / PER; j++)
+      c[j] = __builtin_amdgcn_raw_buffer_load_b128(
+          r, (threadIdx.x + (uint32_t)j * kCountThreads) * 16u, 0, 0);
+#pragma unroll
+    for (int k = 0; k < kCountItems; k++) {
+      const u32x4 v = c[k / PER];
+      if constexpr (KB == 8)
+        raw[k] = (U)((uint64_t)v[2 * (k % PER)] | ((uint64_t)v[2 * (k % PER) + 1] << 32));
+      else
+        raw[k] = (U)v[k % PER];
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < kCountItems; k++) {
+      const int e = elem(k);
+      raw[k] = e < cnt ? (U)gld<KT>(kp + (base + e) * (int64_t)ks) : (U)0;
+    }
   }
   U vor = 0;
   // A wave holds 64 consecutive keys. Sorted or constant inputs give it one
@@ -718,11 +749,11 @@ __global__ __launch_bounds__(kCountThreads) void count_kernel(
   {
     const uint32_t d = pass_digit<LUT>(xf(raw[0]), P.shift, mask, lut);
     const uint32_t d0 = __builtin_amdgcn_readfirstlane(d);
-    agg = __ballot(threadIdx.x < (uint32_t)cnt && d == d0) == __ballot(threadIdx.x < (uint32_t)cnt);
+    agg = __ballot(elem(0) < cnt && d == d0) == __ballot(elem(0) < cnt);
   }
 #pragma unroll
   for (int k = 0; k < kCountItems; k++) {
-    const int e = k * kCountThreads + threadIdx.x;
+    const int e = elem(k);
     const bool ok = e < cnt;
     const U u = xf(raw[k]);
     const uint32_t d = pass_digit<LUT>(u, P.shift, mask, lut);
@@ -1325,21 +1356,25 @@ template <int NT, int IT>
 struct FastLds {
   // sbuf: packed sort words (+ rank sentinels) during the sort, column
   // staging afterwards
+  // (field order: the layout the compiler gave the former separate
+  // __shared__ arrays)
   uint64_t sbuf[NT * IT + kRankSortMax];
   uint16_t perm[NT * IT];                      // output slot -> original index
-  uint32_t hist2[(1 << kLocalTopBits) / 2];    // 16-bit bucket sizes, then cursors (pairs)
   uint16_t bin_start[(1 << kLocalTopBits) + 2];
-  uint32_t scan_sh[NT / 64 + 1];
-  unsigned long long sh_or;
   int maxlen;
+  unsigned long long sh_or;
+  uint32_t hist2[(1 << kLocalTopBits) / 2];    // 16-bit bucket sizes, then cursors (pairs)
+  uint32_t scan_sh[NT / 64 + 1];
 };
 
 // One segment g (<= NT * IT records) by one workgroup. Returns true when the
 // segment goes to the stable path instead (nothing written to global memory
 // then); block-uniform.
-template <typename KT, typename U, int NT, int IT, bool CZ>
+// bail() runs (every thread) right where the segment is handed over: the
+// grid kernel appends it to its fallback list there.
+template <typename KT, typename U, int NT, int IT, bool CZ, typename Bail>
 __device__ __forceinline__ bool local_fast_body(const SortDesc* __restrict__ desc, const Seg g,
-                                                FastLds<NT, IT>& Ls) {
+                                                FastLds<NT, IT>& Ls, Bail bail) {
   constexpr int NW = NT / 64;
   constexpr int CAP = NT * IT;
   constexpr int IDXB = CAP <= 4096 ? 12 : 13;  // bits of an index inside the segment
@@ -1415,7 +1450,8 @@ __device__ __forceinline__ bool local_fast_body(const SortDesc* __restrict__ des
     // to the stable kernel.
     const bool wide = !exact && hi + 1 + IDXB > 64;
     if (wide && sh - lo + IDXB > 64) {
-      return true;  // the stable kernel takes it
+      bail();  // the stable kernel takes it
+      return true;
     }
     const uint64_t below = (sh - lo >= 64) ? ~0ull : ((1ull << (sh - lo)) - 1);
     const uint32_t mask = (1u << nbits) - 1;
@@ -1427,6 +1463,7 @@ __device__ __forceinline__ bool local_fast_body(const SortDesc* __restrict__ des
       // here; no bucket-size limit. Per-wave counters [NW][nb] live in sbuf.
       constexpr bool kWcFits = NW * NB * sizeof(uint16_t) <= CAP * sizeof(uint64_t);
       if constexpr (!kWcFits) {  // (tuning shapes only) the stable kernel takes it
+        bail();
         return true;
       }
       uint16_t* wc = (uint16_t*)sbuf;
@@ -1528,6 +1565,7 @@ __device__ __forceinline__ bool local_fast_body(const SortDesc* __restrict__ des
     if (maxlen > kRankSortMax) {
       // a large bucket (duplicates or skew): local_stable_kernel takes the
       // segment (nothing has been written to global memory yet)
+      bail();
       return true;
     }
 #pragma unroll
@@ -1751,8 +1789,9 @@ __global__ __launch_bounds__(NT, WPE) void local_kernel(const SortDesc* __restri
                                                    unsigned long long* fallback_count) {
   __shared__ FastLds<NT, IT> Ls;
   const Seg g = segs[blockIdx.x];
-  if (local_fast_body<KT, U, NT, IT, CZ>(desc, g, Ls) && threadIdx.x == 0)
-    fallback[atomicAdd(fallback_count, 1ull)] = g;
+  local_fast_body<KT, U, NT, IT, CZ>(desc, g, Ls, [&] {
+    if (threadIdx.x == 0) fallback[atomicAdd(fallback_count, 1ull)] = g;
+  });
 }
 
 // Stable path for segments the fast kernel handed over (a top-digit bucket
@@ -2202,7 +2241,7 @@ __global__ __launch_bounds__(kLocalThreads) void small_sort_kernel(const SortDes
   __shared__ SmallLds Ls;
   const SortDesc* desc = &d;
   int path = 0;
-  if (local_fast_body<KT, U, kLocalThreads, kLocalItems, CZ>(desc, g, Ls.fast)) {
+  if (local_fast_body<KT, U, kLocalThreads, kLocalItems, CZ>(desc, g, Ls.fast, [] {})) {
     __syncthreads();  // the fast body's LDS is reused
     path = 1;
     if (local_stable_body<KT, U, kLocalStableThreads, CZ>(desc, g, Ls.stable)) {
