@@ -2229,6 +2229,8 @@ __global__ __launch_bounds__(kLocalStableThreads) void local_lsd_kernel(
 // the descriptor as a kernel argument. taken[0] / taken[1] record whether the
 // stable / LSD body ran (srs_debug_last_fallbacks).
 static_assert(kLocalStableThreads == kLocalThreads, "the three bodies share one workgroup");
+static_assert(sizeof(SortDesc) + sizeof(Seg) + sizeof(int64_t*) <= 4096,
+              "small_sort_kernel's arguments fit the 4 KB kernel-argument segment");
 union SmallLds {
   FastLds<kLocalThreads, kLocalItems> fast;
   StableLds<kLocalStableThreads> stable;

@@ -241,10 +241,12 @@ def test_local_fallback_paths(case, n):
         assert lsd_n == 0, "the stable kernel should have finished these segments"
 
 
+@pytest.mark.parametrize("n", [5000, 50000], ids=["one-launch", "levels"])
 @pytest.mark.parametrize("sizes", [[1], [2], [4], [8], [8, 1], [4, 4], [8, 8, 8], [1] * 63,
                                    [2, 8, 1, 4]])
-def test_payload_packs(sizes):
-    n = 50000
+def test_payload_packs(sizes, n):
+    # n = 5000: the single-launch small sort, whose descriptor (up to 65
+    # columns) travels as a kernel argument
     keys = make_keys(5, "gaussian", n, 7)
     pays = [payload_of(keys, s, salt=i) for i, s in enumerate(sizes)]
     idx = np.arange(n, dtype=np.uint64)
