@@ -38,6 +38,8 @@ CONFIGS = {
     "c3": ("u64", [8], "aos", "1e9 DataElement<uint64,uint64> combined AoS array"),
     "k64": ("u64", [], "soa", "uint64 keys only (diagnostic)"),
     "k32": ("u32", [], "soa", "uint32 keys only (C0 shape)"),
+    "c2w": ("f32", [8], "soa", "float32 keys + one uint64 payload (C2's 12-byte records, "
+            "payload as one 8-byte column; diagnostic)"),
 }
 
 

@@ -519,7 +519,7 @@ int run_level(Workspace* W, int ks, const SortDesc* d_desc, LevelState& S, int f
 // TMP2 the workspace (AoS records as one column, or as 8-byte slices that are
 // dense SoA columns in the workspace when aos_cols).
 void set_columns(const Request& R, SortDesc& d, char* tmp, char* tmp2, bool aos_cols,
-                 size_t slice_bytes, const size_t* tmp_off, bool inplace) {
+                 size_t slice_bytes, const size_t* tmp_off, bool inplace, bool pair = false) {
   const int ks = key_size_of(R.kind);
   if (R.aos) {
     const uint32_t E = R.elem_size;
@@ -542,7 +542,16 @@ void set_columns(const Request& R, SortDesc& d, char* tmp, char* tmp2, bool aos_
     for (int c = 0; c < R.ncols; c++) {
       const uint32_t w = R.widths[c];
       d.cols[c] = Col{{(char*)R.in_cols[c], (char*)R.out_cols[c], tmp ? tmp + tmp_off[c] : nullptr,
-                       nullptr}, w, {w, w, w, w}};
+                       tmp2 ? tmp2 + tmp_off[c] : nullptr}, w, {w, w, w, w}};
+    }
+    if (pair) {  // payloads 1 and 2: one interleaved 8-byte word column in TMP / TMP2
+      for (int c = 1; c <= 2; c++) {
+        const size_t off = tmp_off[1] + 4 * (c - 1);
+        d.cols[c].base[BUF_TMP] = tmp + off;
+        d.cols[c].base[BUF_TMP2] = tmp2 + off;
+        d.cols[c].stride[BUF_TMP] = d.cols[c].stride[BUF_TMP2] = 8;
+      }
+      d.pair = 1;
     }
     d.key = d.cols[0];
     d.ncols = R.ncols;
@@ -605,6 +614,13 @@ int run_sort(Workspace* W, const Request& R, hipStream_t st) {
   // later count passes then read 8-byte keys instead of whole records and
   // the middle scatters move dense columns
   const bool aos_cols = R.aos && R.elem_size >= 16 && n > kLocalCap && R.nsegs == 0;
+  // A key and two 4-byte payload columns (C2) travel with the payloads
+  // interleaved as one 8-byte word per record through TMP / TMP2: the
+  // scatters then write 64-byte runs of words instead of two columns of
+  // 32-byte runs (the same bytes as one 8-byte payload column measured
+  // 23.6 -> 21.1 ms at 1e9)
+  const bool pair_cols = !R.aos && R.ncols == 3 && R.widths[1] == 4 && R.widths[2] == 4 &&
+                         n > kLocalCap && R.nsegs == 0;
   size_t tmp_bytes = 0, slice_bytes = 0;
   std::vector<size_t> tmp_off;
   if (R.aos) {
@@ -614,19 +630,19 @@ int run_sort(Workspace* W, const Request& R, hipStream_t st) {
   } else {
     for (int c = 0; c < R.ncols; c++) {
       tmp_off.push_back(tmp_bytes);
-      tmp_bytes += align_up((size_t)n * R.widths[c], 256);
+      tmp_bytes += align_up((size_t)n * R.widths[c], 256);  // (a pair: 8n bytes at tmp_off[1])
     }
   }
   SRS_TRY(ensure(W->tmp, tmp_bytes));
   char* tmp = (char*)W->tmp.p;
   char* tmp2 = nullptr;
-  if (aos_cols) {
+  if (aos_cols || pair_cols) {
     SRS_TRY(ensure(W->tmp2, tmp_bytes));
     tmp2 = (char*)W->tmp2.p;
     d.tmp2 = 1;
   }
 
-  set_columns(R, d, tmp, tmp2, aos_cols, slice_bytes, tmp_off.data(), inplace);
+  set_columns(R, d, tmp, tmp2, aos_cols, slice_bytes, tmp_off.data(), inplace, pair_cols);
 
   d.stamp_acc = g_stamp_acc;
   bool balanced = false;

@@ -48,6 +48,10 @@ struct SortDesc {
   int32_t tmp2;            // AoS records as SoA slice columns in TMP / TMP2
                            // (scatters go IN -> TMP, TMP <-> TMP2; the local
                            // pass writes the records back to OUT)
+  int32_t pair;            // SoA key + two 4-byte payloads (C2): cols 1 and 2
+                           // are one interleaved 8-byte word per record in
+                           // TMP / TMP2 (stride 8, col 2 at +4; tmp2 is set),
+                           // separate arrays in IN / OUT
   // transformed key u = bits ^ (bits & signbit ? mneg : mpos)
   uint64_t mpos, mneg, signbit, negzero;
   // partition passes only: digit = digit_lut[u >> lut_shift]

@@ -1084,10 +1084,13 @@ __device__ __forceinline__ TileInfo scatter_load_tile(
   const int ebase = (int)(threadIdx.x >> 6) * IT * 64 + (int)lane_id();
   load_strip<IT>(v0, desc->cols[0].base[P.buf], desc->cols[0].width,
                  desc->cols[0].stride[P.buf], ti.base, ebase, ti.cnt);
+  // (desc->pair: in TMP / TMP2 columns 1 and 2 are one 8-byte word column,
+  // loaded whole into v1)
+  const bool pair_src = PRE3 && desc->pair && (P.buf == BUF_TMP || P.buf == BUF_TMP2);
   if (ncols > 1)
-    load_strip<IT>(v1, desc->cols[1].base[P.buf], desc->cols[1].width,
+    load_strip<IT>(v1, desc->cols[1].base[P.buf], pair_src ? 8u : desc->cols[1].width,
                    desc->cols[1].stride[P.buf], ti.base, ebase, ti.cnt);
-  if (PRE3 && ncols > 2)
+  if (PRE3 && ncols > 2 && !pair_src)
     load_strip<IT>(v2, desc->cols[2].base[P.buf], desc->cols[2].width,
                    desc->cols[2].stride[P.buf], ti.base, ebase, ti.cnt);
   my_off = 0;
@@ -1236,9 +1239,31 @@ __device__ __forceinline__ void scatter_process_tile(
     });
   };
   if constexpr (PRE3) {
-    for (int c = 1; c < ncols; c += 2) {
-      move_col(c, v1);
-      if (c + 1 < ncols) move_col(c + 1, v2);
+    if (desc->pair) {
+      // key + two 4-byte payloads whose destination (TMP / TMP2) holds them as
+      // one interleaved word per record: one staging pass and 8-byte stores
+      // (from IN / OUT, the caller's arrays, the two columns were loaded apart
+      // and are joined here)
+      if (P.buf != BUF_TMP && P.buf != BUF_TMP2) {
+#pragma unroll
+        for (int k = 0; k < IT; k++) v1[k] = (v1[k] & 0xFFFFFFFFull) | (v2[k] << 32);
+      }
+      lds_barrier();
+#pragma unroll
+      for (int k = 0; k < IT; k++)
+        if (valid(k)) L.sval[pos[k]] = v1[k];
+      lds_barrier();
+      char* out = desc->cols[1].base[P.dst];
+#pragma unroll
+      for (int i = 0; i < IT; i++) {
+        const int j = i * NT + (int)threadIdx.x;
+        if (j < cnt) stw<8>(out + ((int64_t)j + L.gdst[dout[i]]) * 8, L.sval[j]);
+      }
+    } else {
+      for (int c = 1; c < ncols; c += 2) {
+        move_col(c, v1);
+        if (c + 1 < ncols) move_col(c + 1, v2);
+      }
     }
   } else {
     for (int c = 1; c < ncols; c++) move_col(c, v1);
@@ -1521,7 +1546,8 @@ __device__ __forceinline__ bool local_fast_body(const SortDesc* __restrict__ des
     // (SoA columns are dense in every buffer: the DIRECT code has no strided
     // load or store path)
     const bool direct = !CZ && !wide && desc->cols[0].width == (uint32_t)kbytes &&
-                        desc->cols[0].stride[BUF_OUT] == (uint32_t)kbytes && !desc->tmp2 &&
+                        desc->cols[0].stride[BUF_OUT] == (uint32_t)kbytes &&
+                        (!desc->tmp2 || desc->pair) &&
                         desc->cols[0].stride[BUF_IN] == (uint32_t)kbytes;
     auto bucket_rank = [&](auto DIRECT_) -> bool {
     constexpr bool DIRECT = decltype(DIRECT_)::value;
@@ -1683,11 +1709,16 @@ __device__ __forceinline__ bool local_fast_body(const SortDesc* __restrict__ des
       // word slot in perm. u = known top bits | word bits, then the inverse
       // key transform. The other columns staged, written in order. FW: the
       // payload width as a compile-time fact for the common one-column case.
+      // FW: the payload width when there is exactly one payload column (0:
+      // any columns, staged one by one; -1: desc->pair's two 4-byte payloads
+      // read as one 8-byte word column from TMP / TMP2)
       auto direct_out = [&](auto FW_) {
         constexpr int FW = decltype(FW_)::value;
         if (ncols > 1) {
-          if constexpr (FW != 0) load_strip<IT, true, FW>(vn, desc->cols[1].base[g.buf], FW, FW,
-                                                          base, ebase, cnt);
+          if constexpr (FW > 0) load_strip<IT, true, FW>(vn, desc->cols[1].base[g.buf], FW, FW,
+                                                         base, ebase, cnt);
+          else if constexpr (FW < 0) load_strip<IT, true, 8>(vn, desc->cols[1].base[g.buf], 8, 8,
+                                                             base, ebase, cnt);
           else load_col_dense(1, vn);
         }
         uint32_t id[IT];
@@ -1703,14 +1734,21 @@ __device__ __forceinline__ bool local_fast_body(const SortDesc* __restrict__ des
                                 return (uint64_t)xf.inv((U)(top | (w >> IDXB)));
                               });
         STAMP();  // 5: column 0 moved
-        if constexpr (FW != 0) {  // exactly one payload column
+        if constexpr (FW != 0) {  // exactly one payload column (or word pair)
           lds_barrier();  // every read of the words is done
 #pragma unroll
           for (int k = 0; k < IT; k++)
             if (valid(k)) sbuf[ebase + k * 64] = vn[k];
           lds_barrier();
-          store_strip<IT, true, FW>(desc->cols[1].base[BUF_OUT], FW, FW, base, ebase, cnt,
-                                    [&](int k) { return sbuf[id[k]]; });
+          if constexpr (FW > 0) {
+            store_strip<IT, true, FW>(desc->cols[1].base[BUF_OUT], FW, FW, base, ebase, cnt,
+                                      [&](int k) { return sbuf[id[k]]; });
+          } else {  // the two halves of each word to their own OUT arrays
+            store_strip<IT, true, 4>(desc->cols[1].base[BUF_OUT], 4, 4, base, ebase, cnt,
+                                     [&](int k) { return sbuf[id[k]] & 0xFFFFFFFFull; });
+            store_strip<IT, true, 4>(desc->cols[2].base[BUF_OUT], 4, 4, base, ebase, cnt,
+                                     [&](int k) { return sbuf[id[k]] >> 32; });
+          }
         } else {
           // column c is staged straight from vn, whose registers then take
           // column c + 1's loads before column c's stores (no register
@@ -1729,6 +1767,8 @@ __device__ __forceinline__ bool local_fast_body(const SortDesc* __restrict__ des
         }
       };
       if (ncols == 2 && desc->cols[1].width == 8) direct_out(std::integral_constant<int, 8>{});
+      else if (desc->pair && (g.buf == BUF_TMP || g.buf == BUF_TMP2))
+        direct_out(std::integral_constant<int, -1>{});
       else direct_out(std::integral_constant<int, 0>{});
       STAMP();  // 6
       STAMP_FLUSH(1);
@@ -1753,7 +1793,11 @@ __device__ __forceinline__ bool local_fast_body(const SortDesc* __restrict__ des
   // staged and stored, so their latency hides behind that work. In place is
   // safe: a column's loads complete before the barrier that precedes its own
   // stores, and different columns never share bytes.
-  if (ncols > 1) load_col(1, vn);
+  // desc->pair with the segment in TMP / TMP2: columns 1 and 2 are one word
+  // column there (one load and staging pass, two half-word store passes)
+  const bool pw = desc->pair && (g.buf == BUF_TMP || g.buf == BUF_TMP2);
+  if (pw) load_strip<IT>(vn, desc->cols[1].base[g.buf], 8, 8, base, ebase, cnt);
+  else if (ncols > 1) load_col(1, vn);
   // column 0 from v0 (the barrier after the perm writes already ordered
   // every earlier sbuf access), then each column c >= 1 staged straight from
   // vn, whose registers take column c + 1's loads before column c's stores
@@ -1766,7 +1810,18 @@ __device__ __forceinline__ bool local_fast_body(const SortDesc* __restrict__ des
                   desc->cols[0].stride[BUF_OUT], base, ebase, cnt,
                   [&](int k) { return sbuf[id[k]]; });
   STAMP();  // 5: column 0 moved
-  for (int c = 1; c < ncols; c++) {
+  if (pw) {
+    lds_barrier();
+#pragma unroll
+    for (int k = 0; k < IT; k++)
+      if (valid(k)) sbuf[ebase + k * 64] = vn[k];
+    lds_barrier();
+    store_strip<IT>(desc->cols[1].base[BUF_OUT], 4, desc->cols[1].stride[BUF_OUT], base, ebase,
+                    cnt, [&](int k) { return sbuf[id[k]] & 0xFFFFFFFFull; });
+    store_strip<IT>(desc->cols[2].base[BUF_OUT], 4, desc->cols[2].stride[BUF_OUT], base, ebase,
+                    cnt, [&](int k) { return sbuf[id[k]] >> 32; });
+  }
+  for (int c = pw ? ncols : 1; c < ncols; c++) {
     lds_barrier();
 #pragma unroll
     for (int k = 0; k < IT; k++)

@@ -367,6 +367,24 @@ def test_device_api_rejects_mismatched_tensors():
         srs_amd.sort_device(k, out=(torch.zeros(100, dtype=torch.int32, device=dev),))
 
 
+@pytest.mark.parametrize("kind", [0, 3, 4, 7, 8, 9], ids=lambda k: KIND_NAMES[k])
+@pytest.mark.parametrize("up", [True, False], ids=["up", "down"])
+def test_two_u32_payloads_travel_as_words(kind, up):
+    """A key and two 4-byte payloads (C2's shape) move through the workspace
+    as one interleaved 8-byte word per record (SortDesc::pair): joined by the
+    first scatter, split by the local pass, copied home apart by the copy
+    list; a payload of input indices checks stability bit for bit."""
+    for di, dist in enumerate(["uniform", "gaussian", "zero", "fewdistinct", "highbits"]):
+        n = 70001 if di else 600_011
+        keys = make_keys(kind, dist, n, 31 * kind + di)
+        p0 = payload_of(keys, 4)
+        p1 = np.arange(n, dtype=np.uint32)
+        k, a, b = keys.copy(), p0.copy(), p1.copy()
+        srs_amd.sort(k, a, b, up=up)
+        st = stable_reference(kind, up, [keys, p0, p1])
+        assert bytes_equal(k, st[0]) and bytes_equal(a, st[1]) and bytes_equal(b, st[2]), dist
+
+
 def test_device_float_keys_two_payloads():
     """C2 shape: f32 keys in [-1, 1) + two u32 payload columns."""
     torch = _torch()
