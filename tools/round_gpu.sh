@@ -13,3 +13,4 @@ bash tools/profile_round.sh $TAG || exit 1
 st bench_c2 400 python bench.py --config c2 --steps 3 --cpu-sample 0
 st bench_c3 400 python bench.py --config c3 --steps 3 --cpu-sample 0
 for f in gpurun_out/prof/$TAG/bench_trace.log gpurun_out/bench_c2.log gpurun_out/bench_c3.log; do python tools/show.py $f | cut -c1-330; done
+st perf_dat 900 python tools/perf_dat.py --out gpurun_out/perf_dat
