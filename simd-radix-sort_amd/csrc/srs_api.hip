@@ -198,6 +198,9 @@ struct Workspace {
   DevBuf plan, tcount, gcount, tbase, gbase, var, sbase;
   DevBuf tile_seg, group_seg, hist, offs, gsum, gofs, scan_tmp, totals, ctr;
   DevBuf shist, lut, lut_rbits;  // balanced first level (sampled histogram, digit table)
+  // stripe first level: piece sizes and tile prefixes, bucket totals, the
+  // second level's tile counts and gathered tile table (GTile)
+  DevBuf prun, ptile, btot, bnt, btile, nt_over, gtile;
   ListCounters* h_ctr = nullptr;
   uint64_t* h_totals = nullptr;
   // Stream order of the workspace: the last call's kernels may still be
@@ -407,8 +410,20 @@ struct LevelState {
 // plan -> bases -> count -> offsets + children -> scatter. Children go to
 // W->big[S.cur ^ 1] / the local lists / the copy list; S is updated from the
 // device counters. force_bits / lut: partition passes (srs_partition_device).
+// How a level reads and hands on its segments: mode 0 plain; 1 a stripe
+// level (its segments are stripes of the input, partitioned each on its own;
+// the next level's segments are the buckets, read through a gathered tile
+// table); 2 that gathered level. See GTile (srs_common.h).
+struct LevelMode {
+  int mode = 0;
+  const GTile* gt = nullptr;        // mode 2
+  const int32_t* nt_over = nullptr; // mode 2: tiles per segment
+  int key_bits = 0;                 // mode 1
+};
+
 int run_level(Workspace* W, int ks, const SortDesc* d_desc, LevelState& S, int force_bits,
-              bool lut, hipStream_t st, const int32_t* lut_rbits = nullptr) {
+              bool lut, hipStream_t st, const int32_t* lut_rbits = nullptr,
+              const LevelMode& M = LevelMode()) {
   const int64_t nbig = S.nbig;
   ListCounters* d_ctr = (ListCounters*)W->ctr.p;
   uint64_t* d_totals = (uint64_t*)W->totals.p;
@@ -428,12 +443,12 @@ int run_level(Workspace* W, int ks, const SortDesc* d_desc, LevelState& S, int f
     TimedScope ts("plan", (double)nbig, st);
     launch_plan_small((Seg*)W->big[S.cur].p, nbig, plan, (int64_t*)W->tbase.p,
                       (int64_t*)W->gbase.p, var, d_totals, &d_ctr->n_big, force_bits, S.tmp2,
-                      st);
+                      st, M.nt_over);
   } else {
     TimedScope ts("plan", (double)nbig, st);
     HIP_TRY(hipMemsetAsync(d_totals + 3, 0, sizeof(uint64_t), st));
     launch_plan((Seg*)W->big[S.cur].p, nbig, plan, (int64_t*)W->tcount.p,
-                (int64_t*)W->gcount.p, var, d_totals + 3, force_bits, S.tmp2, st);
+                (int64_t*)W->gcount.p, var, d_totals + 3, force_bits, S.tmp2, st, M.nt_over);
     launch_excl_scan((uint64_t*)W->tcount.p, (uint64_t*)W->tbase.p, nbig,
                      (uint64_t*)W->scan_tmp.p, d_totals + 0, st);
     launch_excl_scan((uint64_t*)W->gcount.p, (uint64_t*)W->gbase.p, nbig,
@@ -476,7 +491,7 @@ int run_level(Workspace* W, int ks, const SortDesc* d_desc, LevelState& S, int f
                   group_seg, nbig, st);
   {
     TimedScope ts("count", (double)0, st);
-    launch_count(ks, d_desc, plan, tile_seg, ntiles, (uint16_t*)W->hist.p, var, lut, st);
+    launch_count(ks, d_desc, plan, tile_seg, ntiles, (uint16_t*)W->hist.p, var, lut, st, M.gt);
   }
   // ---- offsets + children (list capacity for the worst case: every bin non-empty)
   const size_t worst = (size_t)nbig * kMaxBins;
@@ -493,12 +508,27 @@ int run_level(Workspace* W, int ks, const SortDesc* d_desc, LevelState& S, int f
                    (uint32_t*)W->gsum.p, (uint64_t*)W->gofs.p, (uint64_t*)W->sbase.p,
                    offs32 ? nullptr : (uint64_t*)W->offs.p, offs32 ? (uint32_t*)W->offs.p : nullptr,
                    var, (Seg*)W->big[nxt].p, (Seg*)W->local.p,
-                   (Seg*)W->local2.p, (Seg*)W->copy.p, d_ctr, lut_rbits, st);
+                   (Seg*)W->local2.p, (Seg*)W->copy.p, d_ctr, lut_rbits, st, M.mode,
+                   (uint32_t*)W->prun.p);
   }
   {
     TimedScope ts("scatter", (double)0, st);
     launch_scatter(ks, d_desc, plan, tile_seg, (uint64_t*)W->offs.p,
-                   offs32 ? (const uint32_t*)W->offs.p : nullptr, ntiles, lut, S.ncols, st);
+                   offs32 ? (const uint32_t*)W->offs.p : nullptr, ntiles, lut, S.ncols, st,
+                   M.gt);
+  }
+  if (M.mode == 1) {
+    // the buckets become the next level's segments (logical starts: where
+    // they end up), their tiles the pieces every stripe holds of them
+    // (a digit-table level consumes no fixed bits: its groups' prefixes
+    // come from lut_rbits)
+    const int nb = 1 << std::abs(force_bits);
+    const int rbits = lut ? M.key_bits : M.key_bits - std::abs(force_bits);
+    launch_stripe_tables((const uint32_t*)W->prun.p, nbig, nb, (uint32_t*)W->ptile.p,
+                         (uint64_t*)W->btot.p, (uint32_t*)W->bnt.p, rbits, BUF_TMP,
+                         (Seg*)W->big[nxt].p, (int32_t*)W->nt_over.p, (uint32_t*)W->btile.p,
+                         d_ctr, (const uint64_t*)W->sbase.p, plan, (GTile*)W->gtile.p,
+                         lut_rbits, st);
   }
   HIP_TRY(hipMemcpyAsync(W->h_ctr, d_ctr, sizeof(ListCounters), hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
@@ -592,6 +622,16 @@ int run_small(Workspace* W, const Request& R, hipStream_t st) {
   }
   HIP_TRY(hipGetLastError());
   return SRS_OK;
+}
+
+constexpr int64_t kStripeMinN = int64_t(1) << 25;
+
+bool stripes_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("SRS_NO_STRIPES");
+    return !(e && *e && *e != '0');
+  }();
+  return on;
 }
 
 int run_sort(Workspace* W, const Request& R, hipStream_t st) {
@@ -722,7 +762,54 @@ int run_sort(Workspace* W, const Request& R, hipStream_t st) {
   LevelState S{n_big, n_local, n_local2, n_copy, 0, d.ncols, d.tmp2};
   if (R.nsegs == 0 && n_big == 1) S.known_len = n;
   int level = 0;
-  if (balanced && S.nbig > 0) {
+  // Stripe first level: large plain SoA sorts partition
+  // stripes of kStripeKeysPerBucket << b1 keys on their own with the first
+  // digit, so a tile's scattered runs land in its stripe's window (the
+  // second level's scatter, which writes into one bucket's window, measured
+  // 5.9 ms per C1 launch against 7.0 for the first one over the whole array)
+  // (a balanced first level: its 512 digit-table groups are the buckets)
+  const int b1 = balanced ? kMaxDigitBits : choose_bits(n, d.key_bits);
+  const int64_t stripe_len = (int64_t)kStripeKeysPerBucket << b1;
+  const bool stripes = R.nsegs == 0 && !d.canon_zero && (ks == 4 || ks == 8) &&
+                       n >= kStripeMinN && n < (int64_t(1) << 32) && n >= 2 * stripe_len &&
+                       stripes_enabled();
+  if (stripes) {
+    const int64_t K = (n + stripe_len - 1) / stripe_len;
+    std::vector<Seg> hs(K);
+    for (int64_t k = 0; k < K; k++)
+      hs[k] = Seg{k * stripe_len, std::min(stripe_len, n - k * stripe_len), d.key_bits, home};
+    SRS_TRY(ensure(W->big[0], K * sizeof(Seg)));
+    HIP_TRY(hipMemcpyAsync(W->big[0].p, hs.data(), K * sizeof(Seg), hipMemcpyHostToDevice, st));
+    const int nb = 1 << b1;
+    const size_t pieces = (size_t)K * kMaxBins;
+    SRS_TRY(ensure(W->prun, pieces * 4));
+    SRS_TRY(ensure(W->ptile, pieces * 4));
+    SRS_TRY(ensure(W->btot, kMaxBins * 8));
+    SRS_TRY(ensure(W->bnt, kMaxBins * 4));
+    SRS_TRY(ensure(W->btile, kMaxBins * 4));
+    SRS_TRY(ensure(W->nt_over, kMaxBins * 4));
+    // tiles of the gathered level: at most one partial tile per piece
+    SRS_TRY(ensure(W->gtile, ((n + kTile - 1) / kTile + (size_t)K * nb) * sizeof(GTile)));
+    HIP_TRY(hipStreamSynchronize(st));  // hs goes out of scope
+    S.nbig = K;
+    S.known_len = -1;
+    LevelMode m1;
+    m1.mode = 1;
+    m1.key_bits = d.key_bits;
+    ++level;
+    if (balanced)
+      SRS_TRY(run_level(W, ksl, d_desc, S, kMaxDigitBits, true, st,
+                        (const int32_t*)W->lut_rbits.p, m1));
+    else
+      SRS_TRY(run_level(W, ksl, d_desc, S, -b1, false, st, nullptr, m1));
+    LevelMode m2;
+    m2.mode = 2;
+    m2.gt = (const GTile*)W->gtile.p;
+    m2.nt_over = (const int32_t*)W->nt_over.p;
+    ++level;
+    if (S.nbig > 0) SRS_TRY(run_level(W, ksl, d_desc, S, 0, false, st, nullptr, m2));
+  }
+  if (balanced && !stripes && S.nbig > 0) {
     ++level;
     SRS_TRY(run_level(W, ksl, d_desc, S, kMaxDigitBits, true, st,
                       (const int32_t*)W->lut_rbits.p));

@@ -12,6 +12,7 @@
 // partition (BitSorterSIMD::sortBit, radixSort.hpp:1587-1686).
 #pragma once
 
+#include <hip/hip_runtime.h>
 #include <stdint.h>
 
 namespace srs {
@@ -84,6 +85,24 @@ struct SegPlan {
   int32_t dst;        // destination buffer of the scatter
   int32_t skip;       // set by the children kernel: one bucket holds everything
 };
+
+// Stripe first level: the first digit partitions each stripe
+// of kStripeKeysPerBucket << bits keys on its own, so a tile's scattered runs
+// land in the stripe's window instead of across the whole array; bucket b's
+// pieces (one per stripe, in stripe order) are then read by the second level
+// through a table of gathered tiles: tile t of that level holds the cnt
+// records at element src of its source buffer (never straddling a piece).
+struct GTile {
+  int64_t src;
+  int32_t cnt;
+  int32_t pad;
+};
+// average piece (one stripe's share of one bucket) for uniform keys: 95 % of
+// a tile, so a piece almost never spills a second, nearly empty tile
+#ifndef SRS_STRIPE_KPB
+#define SRS_STRIPE_KPB 3904
+#endif
+constexpr int kStripeKeysPerBucket = SRS_STRIPE_KPB;
 
 // Work-list counters (device), read back by the host once per level.
 struct ListCounters {
@@ -181,5 +200,31 @@ constexpr int kLocalTarget = 6144;                        // digit sizing target
 #define SRS_LOCAL_SMALL_TARGET 3840
 #endif
 constexpr int kLocalSmallTarget = SRS_LOCAL_SMALL_TARGET;
+
+// Digit width for a segment of `len` keys with `rbits` unsorted bits: as many
+// bits as needed to bring buckets under kLocalTarget, spread evenly over the
+// levels that will take, at most kMaxDigitBits per level. (Host and device:
+// the host sizes the stripe level with it.)
+__host__ __device__ inline int levels_for(int64_t len, int64_t target, int* need_out) {
+  int need = 1;
+  while (need < 62 && (target << need) < len) need++;
+  *need_out = need;
+  return (need + kMaxDigitBits - 1) / kMaxDigitBits;
+}
+
+__host__ __device__ inline int choose_bits(int64_t len, int rbits) {
+  // bits needed to bring buckets under kLocalTarget, spread evenly over the
+  // levels that takes (<= kMaxDigitBits each); one more bit when that lands
+  // the buckets in the smaller (faster) LDS class without an extra level
+  int need, need_small;
+  const int levels = levels_for(len, kLocalTarget, &need);
+  const int levels_small = levels_for(len, kLocalSmallTarget, &need_small);
+  if (levels_small == levels) need = need_small;
+  int bits = (need + levels - 1) / levels;
+  if (bits > kMaxDigitBits) bits = kMaxDigitBits;
+  if (bits > rbits) bits = rbits;
+  if (bits < 1) bits = 1;
+  return bits;
+}
 
 }  // namespace srs

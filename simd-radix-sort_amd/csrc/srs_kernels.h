@@ -10,11 +10,11 @@ namespace srs {
 
 void launch_plan(const Seg* big, int64_t nbig, SegPlan* plan, int64_t* tcount,
                  int64_t* gcount, unsigned long long* var_or, uint64_t* elems, int force_bits,
-                 int tmp2, hipStream_t st);
+                 int tmp2, hipStream_t st, const int32_t* nt_over = nullptr);
 void launch_plan_small(const Seg* big, int64_t nbig, SegPlan* plan, int64_t* tbase,
                        int64_t* gbase, unsigned long long* var_or, uint64_t* totals,
                        unsigned long long* n_big_next, int force_bits, int tmp2,
-                       hipStream_t st);
+                       hipStream_t st, const int32_t* nt_over = nullptr);
 constexpr int64_t kPlanSmallMax = 16384;  // plan_small_kernel: one workgroup loops over these
 void launch_seg_map2(const int64_t* tbase, int64_t ntiles, int32_t* tile_seg,
                      const int64_t* gbase, int64_t ngroups, int32_t* group_seg, int64_t nbig,
@@ -25,7 +25,8 @@ void launch_plan_bases(SegPlan* plan, int64_t nbig, const int64_t* tbase,
                        const int64_t* gbase, hipStream_t st);
 void launch_count(int key_size, const SortDesc* d, const SegPlan* plan,
                   const int32_t* tile_seg, int64_t ntiles, uint16_t* hist,
-                  unsigned long long* var_or, bool lut, hipStream_t st);
+                  unsigned long long* var_or, bool lut, hipStream_t st,
+                  const GTile* gt = nullptr);
 int64_t scan_temp_elems(int64_t n);
 void launch_excl_scan(const uint64_t* x, uint64_t* y, int64_t n, uint64_t* temp,
                       uint64_t* total, hipStream_t st);
@@ -33,10 +34,19 @@ void launch_offsets(SegPlan* plan, int64_t nbig, const int32_t* group_seg, int64
                     const uint16_t* hist, uint32_t* gsum, uint64_t* gofs, uint64_t* sbase,
                     uint64_t* offs, uint32_t* offs32, const unsigned long long* var_or,
                     Seg* big_next, Seg* local, Seg* local2, Seg* copy, ListCounters* ctr,
-                    const int32_t* lut_rbits, hipStream_t st);
+                    const int32_t* lut_rbits, hipStream_t st, int mode = 0,
+                    uint32_t* prun = nullptr);
 void launch_scatter(int key_size, const SortDesc* d, const SegPlan* plan,
                     const int32_t* tile_seg, const uint64_t* offs, const uint32_t* offs32,
-                    int64_t ntiles, bool lut, int ncols, hipStream_t st);
+                    int64_t ntiles, bool lut, int ncols, hipStream_t st,
+                    const GTile* gt = nullptr);
+// stripe first level -> the second level's segment list (W->big, n_big),
+// tile counts (nt_over) and gathered tile table (gt); see GTile
+void launch_stripe_tables(const uint32_t* prun, int64_t nstripes, int nb, uint32_t* ptile,
+                          uint64_t* btot, uint32_t* bnt, int rbits, int buf, Seg* big,
+                          int32_t* nt_over, uint32_t* btile, ListCounters* ctr,
+                          const uint64_t* sbase, const SegPlan* plan, GTile* gt,
+                          const int32_t* lut_rbits, hipStream_t st);
 void launch_key_hist(int key_size, int64_t n, const void* keys, const SortDesc& d, int bits,
                      unsigned long long* hist, hipStream_t st);
 void launch_local(int key_size, const SortDesc* d, const Seg* segs, int64_t nsegs, int big_class,

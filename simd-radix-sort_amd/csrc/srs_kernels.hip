@@ -458,32 +458,11 @@ __device__ __forceinline__ void wlms_rank(const uint32_t (&dig)[ITEMS],
 // plan / bookkeeping kernels
 // ---------------------------------------------------------------------------
 
-// Digit width for a segment of `len` keys with `rbits` unsorted bits: as many
-// bits as needed to bring buckets under kLocalTarget, spread evenly over the
-// levels that will take, at most kMaxDigitBits per level.
-__device__ __forceinline__ int levels_for(int64_t len, int64_t target, int* need_out) {
-  int need = 1;
-  while (need < 62 && (target << need) < len) need++;
-  *need_out = need;
-  return (need + kMaxDigitBits - 1) / kMaxDigitBits;
-}
+// (choose_bits: srs_common.h, shared with the host)
 
-__device__ __forceinline__ int choose_bits(int64_t len, int rbits) {
-  // bits needed to bring buckets under kLocalTarget, spread evenly over the
-  // levels that takes (<= kMaxDigitBits each); one more bit when that lands
-  // the buckets in the smaller (faster) LDS class without an extra level
-  int need, need_small;
-  const int levels = levels_for(len, kLocalTarget, &need);
-  const int levels_small = levels_for(len, kLocalSmallTarget, &need_small);
-  if (levels_small == levels) need = need_small;
-  int bits = (need + levels - 1) / levels;
-  if (bits > kMaxDigitBits) bits = kMaxDigitBits;
-  if (bits > rbits) bits = rbits;
-  if (bits < 1) bits = 1;
-  return bits;
-}
-
-__device__ __forceinline__ SegPlan make_plan(const Seg& g, int force_bits, int tmp2) {
+// nt_over (gathered level): the segment's tile count from its tile table
+__device__ __forceinline__ SegPlan make_plan(const Seg& g, int force_bits, int tmp2,
+                                             const int32_t* nt_over = nullptr, int64_t s = 0) {
   SegPlan p;
   p.start = g.start;
   p.len = g.len;
@@ -492,7 +471,7 @@ __device__ __forceinline__ SegPlan make_plan(const Seg& g, int force_bits, int t
   // top-bit ranges)
   p.bits = force_bits ? (force_bits > 0 ? force_bits : -force_bits) : choose_bits(g.len, g.rbits);
   p.shift = force_bits > 0 ? g.rbits : g.rbits - p.bits;
-  p.ntiles = (int32_t)((g.len + kTile - 1) / kTile);
+  p.ntiles = nt_over ? nt_over[s] : (int32_t)((g.len + kTile - 1) / kTile);
   p.ngroups = (p.ntiles + kScanGroup - 1) / kScanGroup;
   p.buf = g.buf;
   // the last scatter lands in OUT (the local pass then sorts in place); with
@@ -510,12 +489,13 @@ __global__ void plan_kernel(const Seg* __restrict__ big, int64_t nbig,
                             SegPlan* __restrict__ plan, int64_t* __restrict__ tcount,
                             int64_t* __restrict__ gcount,
                             unsigned long long* __restrict__ var_or,
-                            uint64_t* __restrict__ elems, int force_bits, int tmp2) {
+                            uint64_t* __restrict__ elems, int force_bits, int tmp2,
+                            const int32_t* __restrict__ nt_over) {
   const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= nbig) return;
   const Seg g = big[s];
   atomicAdd((unsigned long long*)elems, (unsigned long long)g.len);
-  const SegPlan p = make_plan(g, force_bits, tmp2);
+  const SegPlan p = make_plan(g, force_bits, tmp2, nt_over, s);
   plan[s] = p;
   tcount[s] = p.ntiles;
   gcount[s] = p.ngroups;
@@ -532,7 +512,8 @@ __global__ __launch_bounds__(kPlanSmallThreads) void plan_small_kernel(
     const Seg* __restrict__ big, int64_t nbig, SegPlan* __restrict__ plan,
     int64_t* __restrict__ tbase, int64_t* __restrict__ gbase,
     unsigned long long* __restrict__ var_or, uint64_t* __restrict__ totals,
-    unsigned long long* __restrict__ n_big_next, int force_bits, int tmp2) {
+    unsigned long long* __restrict__ n_big_next, int force_bits, int tmp2,
+    const int32_t* __restrict__ nt_over) {
   constexpr int NT = kPlanSmallThreads;
   __shared__ uint64_t sh[3][NT / 64 + 1];
   uint64_t tc = 0, gc = 0, ec = 0;
@@ -542,7 +523,7 @@ __global__ __launch_bounds__(kPlanSmallThreads) void plan_small_kernel(
     uint64_t nt = 0, ng = 0, len = 0;
     if (s < nbig) {
       const Seg g = big[s];
-      p = make_plan(g, force_bits, tmp2);
+      p = make_plan(g, force_bits, tmp2, nt_over, s);
       nt = (uint64_t)p.ntiles;
       ng = (uint64_t)p.ngroups;
       len = (uint64_t)g.len;
@@ -678,7 +659,7 @@ template <typename KT, typename U, bool LUT, bool CZ>
 __global__ __launch_bounds__(kCountThreads) void count_kernel(
     const SortDesc* __restrict__ desc, const SegPlan* __restrict__ plan,
     const int32_t* __restrict__ tile_seg, uint16_t* __restrict__ hist,
-    unsigned long long* __restrict__ var_or) {
+    unsigned long long* __restrict__ var_or, const GTile* __restrict__ gt) {
   __shared__ uint32_t h[kMaxBins];
   __shared__ unsigned long long sh_or;
   const int64_t t = xcd_remap(blockIdx.x, gridDim.x);
@@ -698,10 +679,19 @@ __global__ __launch_bounds__(kCountThreads) void count_kernel(
   if (threadIdx.x == 0) sh_or = 0;
   __syncthreads();
 
-  const int64_t base = P.start + tl * kTile;
-  const int64_t rem = P.len - tl * kTile;
-  const int cnt = rem < kTile ? (int)rem : kTile;
-  const U uref = xf((U)gld<KT>(kp + P.start * (int64_t)ks));
+  int64_t base, first;
+  int cnt;
+  if (gt) {  // gathered level: the tile table says where the records are
+    base = gt[t].src;
+    cnt = gt[t].cnt;
+    first = gt[P.tile_base].src;  // one reference key per segment
+  } else {
+    base = P.start + tl * kTile;
+    const int64_t rem = P.len - tl * kTile;
+    cnt = rem < kTile ? (int)rem : kTile;
+    first = P.start;
+  }
+  const U uref = xf((U)gld<KT>(kp + first * (int64_t)ks));
   U raw[kCountItems];
   // element of item k: a dense 4/8-byte key column is read in 16-byte pieces
   // (range-checked buffer loads; piece j of thread i holds elements
@@ -948,7 +938,12 @@ __global__ __launch_bounds__(kMaxBins) void seg_scan_kernel(
     SegPlan* __restrict__ plan, const uint32_t* __restrict__ gsum,
     uint64_t* __restrict__ gofs, uint64_t* __restrict__ sbase,
     const unsigned long long* __restrict__ var_or, Seg* big_next, Seg* local, Seg* local2,
-    Seg* copy, ListCounters* ctr, const int32_t* __restrict__ lut_rbits) {
+    Seg* copy, ListCounters* ctr, const int32_t* __restrict__ lut_rbits, int mode,
+    uint32_t* __restrict__ prun) {
+  // mode 0: a plain level. 1: a stripe level (every stripe is scattered, its
+  // bucket sizes go to prun; the next level's segments come from
+  // stripe_segs_kernel). 2: a gathered level (every segment is scattered:
+  // its records are not where a skipped segment would have to be).
   __shared__ uint64_t scan_sh[kMaxBins / 64 + 1];
   __shared__ int single;
   const int64_t s = blockIdx.x;
@@ -977,7 +972,11 @@ __global__ __launch_bounds__(kMaxBins) void seg_scan_kernel(
   uint64_t tot;
   const uint64_t ex = block_excl_scan<kMaxBins>(run, scan_sh, &tot);
   if (b < nb) sbase[s * kMaxBins + b] = ex;
-  if (b < nb && (int64_t)run == P.len) single = 1;
+  if (b < nb && (int64_t)run == P.len && mode == 0) single = 1;
+  if (mode == 1) {
+    if (b < nb) prun[s * kMaxBins + b] = (uint32_t)run;
+    return;
+  }
   __syncthreads();
   Seg c;
   c.len = 0;
@@ -1041,6 +1040,89 @@ __global__ __launch_bounds__(kMaxBins) void tile_offs_kernel(
 }
 
 // ---------------------------------------------------------------------------
+// stripe first level -> the second level's segments and gathered tiles
+// ---------------------------------------------------------------------------
+// Piece (s, b): stripe s's share of bucket b, prun[s][b] records at element
+// plan[s].start + sbase[s][b] of the stripe level's destination buffer.
+// Tiles never straddle a piece: piece (s, b) gives ceil(len / kTile) tiles.
+// One block per bucket: per-piece tile prefix (ptile), the bucket's records
+// and tiles (btot, bnt).
+constexpr int kStripeThreads = 256;
+__global__ __launch_bounds__(kStripeThreads) void stripe_tiles_kernel(
+    const uint32_t* __restrict__ prun, int64_t nstripes, uint32_t* __restrict__ ptile,
+    uint64_t* __restrict__ btot, uint32_t* __restrict__ bnt) {
+  __shared__ uint64_t sh[kStripeThreads / 64 + 1];
+  __shared__ uint64_t sh2[kStripeThreads / 64 + 1];
+  const int b = blockIdx.x;
+  uint64_t tiles = 0, keys = 0;
+  for (int64_t s0 = 0; s0 < nstripes; s0 += kStripeThreads) {
+    const int64_t s = s0 + threadIdx.x;
+    const uint32_t len = s < nstripes ? prun[s * kMaxBins + b] : 0u;
+    const uint64_t nt = (len + kTile - 1) / kTile;
+    uint64_t tt, kt;
+    const uint64_t ex = block_excl_scan<kStripeThreads>(nt, sh, &tt);
+    block_excl_scan<kStripeThreads>((uint64_t)len, sh2, &kt);
+    if (s < nstripes) ptile[s * kMaxBins + b] = (uint32_t)(tiles + ex);
+    tiles += tt;
+    keys += kt;
+  }
+  if (threadIdx.x == 0) {
+    btot[b] = keys;
+    bnt[b] = (uint32_t)tiles;
+  }
+}
+
+// One block of kMaxBins threads (thread = bucket): the non-empty buckets
+// become the next level's segments (logical start = records in lower
+// buckets, still `rbits` bits to sort, living in `buf`), with their tile
+// counts (nt_over) and first tiles (btile, per bucket); n_big is set.
+__global__ __launch_bounds__(kMaxBins) void stripe_segs_kernel(
+    const uint64_t* __restrict__ btot, const uint32_t* __restrict__ bnt, int nb, int rbits,
+    int buf, Seg* __restrict__ big, int32_t* __restrict__ nt_over,
+    uint32_t* __restrict__ btile, ListCounters* __restrict__ ctr,
+    const int32_t* __restrict__ lut_rbits) {
+  __shared__ uint64_t sh[3][kMaxBins / 64 + 1];
+  const int b = threadIdx.x;
+  const uint64_t len = b < nb ? btot[b] : 0;
+  const uint64_t nt = b < nb ? bnt[b] : 0;
+  const uint64_t used = len > 0 ? 1 : 0;
+  uint64_t tot_len, tot_nt, tot_used;
+  const uint64_t start = block_excl_scan<kMaxBins>(len, sh[0], &tot_len);
+  const uint64_t tb = block_excl_scan<kMaxBins>(nt, sh[1], &tot_nt);
+  const uint64_t idx = block_excl_scan<kMaxBins>(used, sh[2], &tot_used);
+  if (b < nb) btile[b] = (uint32_t)tb;
+  if (used) {
+    // a digit-table level's group b is a key range whose keys share a prefix
+    const int rb = (lut_rbits && lut_rbits[b] < rbits) ? lut_rbits[b] : rbits;
+    big[idx] = Seg{(int64_t)start, (int64_t)len, rb, buf};
+    nt_over[idx] = (int32_t)nt;
+  }
+  if (b == 0) ctr->n_big = tot_used;
+}
+
+// One thread per piece: its tiles' table entries (bucket-major, then stripe
+// order, so a bucket's tiles list its records in input order: stable).
+__global__ void stripe_gtile_kernel(const uint32_t* __restrict__ prun,
+                                    const uint32_t* __restrict__ ptile,
+                                    const uint32_t* __restrict__ btile,
+                                    const uint64_t* __restrict__ sbase,
+                                    const SegPlan* __restrict__ plan, int64_t nstripes, int nb,
+                                    GTile* __restrict__ gt) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nstripes * nb) return;
+  const int64_t s = i / nb;
+  const int b = (int)(i % nb);
+  const uint32_t len = prun[s * kMaxBins + b];
+  if (len == 0) return;
+  const int64_t src = plan[s].start + (int64_t)sbase[s * kMaxBins + b];
+  GTile* out = gt + btile[b] + ptile[s * kMaxBins + b];
+  for (uint32_t c = 0; c * (uint32_t)kTile < len; c++) {
+    const uint32_t rem = len - c * (uint32_t)kTile;
+    out[c] = GTile{src + (int64_t)c * kTile, (int32_t)(rem < (uint32_t)kTile ? rem : kTile), 0};
+  }
+}
+
+// ---------------------------------------------------------------------------
 // scatter: rank one tile by digit, stage in LDS, write coalesced runs
 // ---------------------------------------------------------------------------
 // Column 0 holds the key in its low bytes (SoA: the key column; AoS: the
@@ -1071,16 +1153,22 @@ template <typename KT, typename U, bool PRE3>
 __device__ __forceinline__ TileInfo scatter_load_tile(
     const SortDesc* __restrict__ desc, const SegPlan* __restrict__ plan,
     const int32_t* __restrict__ tile_seg, const uint64_t* __restrict__ offs,
-    const uint32_t* __restrict__ offs32, int64_t t, int ncols, uint64_t (&v0)[kScatterItems],
-    uint64_t (&v1)[kScatterItems], uint64_t (&v2)[kScatterItems], int64_t& my_off) {
+    const uint32_t* __restrict__ offs32, const GTile* __restrict__ gt, int64_t t, int ncols,
+    uint64_t (&v0)[kScatterItems], uint64_t (&v1)[kScatterItems],
+    uint64_t (&v2)[kScatterItems], int64_t& my_off) {
   constexpr int IT = kScatterItems;
   TileInfo ti;
   ti.s = tile_seg[t];
   const SegPlan P = plan[ti.s];
-  const int64_t tl = t - P.tile_base;
-  ti.base = P.start + tl * kTile;
-  const int64_t rem = P.len - tl * kTile;
-  ti.cnt = P.skip ? 0 : (rem < kTile ? (int)rem : kTile);
+  if (gt) {  // gathered level (never skipped)
+    ti.base = gt[t].src;
+    ti.cnt = gt[t].cnt;
+  } else {
+    const int64_t tl = t - P.tile_base;
+    ti.base = P.start + tl * kTile;
+    const int64_t rem = P.len - tl * kTile;
+    ti.cnt = P.skip ? 0 : (rem < kTile ? (int)rem : kTile);
+  }
   const int ebase = (int)(threadIdx.x >> 6) * IT * 64 + (int)lane_id();
   load_strip<IT>(v0, desc->cols[0].base[P.buf], desc->cols[0].width,
                  desc->cols[0].stride[P.buf], ti.base, ebase, ti.cnt);
@@ -1177,6 +1265,20 @@ __device__ __forceinline__ void scatter_process_tile(
   lds_barrier();
   STAMP();  // 4: column 0 staged
 
+#ifdef SRS_DIAG_WIN
+  // diagnostic (wrong result): each window of SRS_DIAG_WIN consecutive tiles
+  // of a segment is its own little bucket array, so the scattered runs land
+  // in a window of SRS_DIAG_WIN * kTile records instead of the whole segment
+  auto diag_win = [&](int j, uint32_t d) -> int64_t {
+    constexpr int S = SRS_DIAG_WIN;
+    const int64_t tl = (ti.base - P.start) / kTile;
+    const int64_t wb = P.start + (tl / S) * S * kTile;
+    const int64_t per = (int64_t)S * kTile >> P.bits;
+    const int64_t r = ((tl % S) * (per / S) + (j - (int)L.bin_start[d])) % per;
+    const int64_t a = wb + (int64_t)d * per + r;
+    return a < P.start + P.len ? a : ti.base + j;
+  };
+#endif
   // column 0: output slot j's bucket was staged with it
   uint16_t dout[IT];
   {
@@ -1195,6 +1297,8 @@ __device__ __forceinline__ void scatter_process_tile(
           dout[i] = (uint16_t)d;
           #ifdef SRS_DIAG_SEQW
           stw<decltype(W_)::value>(out + ((int64_t)j + ti.base) * (int64_t)st, x);
+#elif defined(SRS_DIAG_WIN)
+          stw<decltype(W_)::value>(out + diag_win(j, d) * (int64_t)st, x);
 #else
           stw<decltype(W_)::value>(out + ((int64_t)j + L.gdst[d]) * (int64_t)st, x);
 #endif
@@ -1231,6 +1335,8 @@ __device__ __forceinline__ void scatter_process_tile(
         if (j < cnt)
           #ifdef SRS_DIAG_SEQW
           stw<decltype(W_)::value>(out + ((int64_t)j + ti.base) * (int64_t)cst, L.sval[j]);
+#elif defined(SRS_DIAG_WIN)
+          stw<decltype(W_)::value>(out + diag_win(j, dout[i]) * (int64_t)cst, L.sval[j]);
 #else
           stw<decltype(W_)::value>(out + ((int64_t)j + L.gdst[dout[i]]) * (int64_t)cst,
                                    L.sval[j]);
@@ -1277,14 +1383,14 @@ template <typename KT, typename U, bool LUT, bool CZ, bool PRE3>
 __global__ __launch_bounds__(kScatterThreads, SRS_SCATTER_WAVES_PER_EU) void scatter_kernel(
     const SortDesc* __restrict__ desc, const SegPlan* __restrict__ plan,
     const int32_t* __restrict__ tile_seg, const uint64_t* __restrict__ offs,
-    const uint32_t* __restrict__ offs32) {
+    const uint32_t* __restrict__ offs32, const GTile* __restrict__ gt) {
   __shared__ ScatterLds<LUT> L;
   __shared__ alignas(16) uint16_t slut[LUT ? kLdsLutEntries : 8];
   const int64_t t = xcd_remap(blockIdx.x, gridDim.x);
   const int ncols = desc->ncols;
   uint64_t v0[kScatterItems], v1[kScatterItems], v2[kScatterItems];
   int64_t my_off;
-  const TileInfo ti = scatter_load_tile<KT, U, PRE3>(desc, plan, tile_seg, offs, offs32, t,
+  const TileInfo ti = scatter_load_tile<KT, U, PRE3>(desc, plan, tile_seg, offs, offs32, gt, t,
                                                      ncols, v0, v1, v2, my_off);
   if (ti.cnt == 0) return;
   // (the table is published by the barrier at the top of the tile)
@@ -2427,17 +2533,18 @@ __global__ void fill_kernel(int64_t n, int kind, uint64_t seed, uint64_t first,
 
 void launch_plan(const Seg* big, int64_t nbig, SegPlan* plan, int64_t* tcount,
                  int64_t* gcount, unsigned long long* var_or, uint64_t* elems, int force_bits,
-                 int tmp2, hipStream_t st) {
+                 int tmp2, hipStream_t st, const int32_t* nt_over) {
   plan_kernel<<<(unsigned)((nbig + 255) / 256), 256, 0, st>>>(
-      big, nbig, plan, tcount, gcount, var_or, elems, force_bits, tmp2);
+      big, nbig, plan, tcount, gcount, var_or, elems, force_bits, tmp2, nt_over);
 }
 
 void launch_plan_small(const Seg* big, int64_t nbig, SegPlan* plan, int64_t* tbase,
                        int64_t* gbase, unsigned long long* var_or, uint64_t* totals,
                        unsigned long long* n_big_next, int force_bits, int tmp2,
-                       hipStream_t st) {
+                       hipStream_t st, const int32_t* nt_over) {
   plan_small_kernel<<<1, kPlanSmallThreads, 0, st>>>(big, nbig, plan, tbase, gbase, var_or,
-                                                     totals, n_big_next, force_bits, tmp2);
+                                                     totals, n_big_next, force_bits, tmp2,
+                                                     nt_over);
 }
 
 void launch_plan_bases(SegPlan* plan, int64_t nbig, const int64_t* tbase,
@@ -2457,14 +2564,14 @@ void launch_seg_map2(const int64_t* tbase, int64_t ntiles, int32_t* tile_seg,
 
 void launch_count(int key_size, const SortDesc* d, const SegPlan* plan,
                   const int32_t* tile_seg, int64_t ntiles, uint16_t* hist,
-                  unsigned long long* var_or, bool lut, hipStream_t st) {
+                  unsigned long long* var_or, bool lut, hipStream_t st, const GTile* gt) {
 #define CALL(KT, U, CZ)                                                                 \
   if (lut)                                                                              \
     count_kernel<KT, U, true, CZ><<<(unsigned)ntiles, kCountThreads, 0, st>>>(            \
-        d, plan, tile_seg, hist, var_or);                                               \
+        d, plan, tile_seg, hist, var_or, gt);                                           \
   else                                                                                  \
     count_kernel<KT, U, false, CZ><<<(unsigned)ntiles, kCountThreads, 0, st>>>(           \
-        d, plan, tile_seg, hist, var_or)
+        d, plan, tile_seg, hist, var_or, gt)
   SRS_KEY_DISPATCH(key_size, CALL)
 #undef CALL
 }
@@ -2484,34 +2591,47 @@ void launch_offsets(SegPlan* plan, int64_t nbig, const int32_t* group_seg, int64
                     uint64_t* offs, uint32_t* offs32, const unsigned long long* var_or,
                     Seg* big_next,
                     Seg* local, Seg* local2, Seg* copy, ListCounters* ctr,
-                    const int32_t* lut_rbits, hipStream_t st) {
+                    const int32_t* lut_rbits, hipStream_t st, int mode, uint32_t* prun) {
   group_sum_kernel<<<(unsigned)ngroups, kMaxBins, 0, st>>>(plan, group_seg, hist, gsum);
   seg_scan_kernel<<<(unsigned)nbig, kMaxBins, 0, st>>>(plan, gsum, gofs, sbase, var_or,
                                                       big_next, local, local2, copy, ctr,
-                                                      lut_rbits);
+                                                      lut_rbits, mode, prun);
   tile_offs_kernel<<<(unsigned)ngroups, kMaxBins, 0, st>>>(
       plan, group_seg, hist, gofs, sbase, offs, offs32);
 }
 
 void launch_scatter(int key_size, const SortDesc* d, const SegPlan* plan,
                     const int32_t* tile_seg, const uint64_t* offs, const uint32_t* offs32,
-                    int64_t ntiles, bool lut, int ncols, hipStream_t st) {
+                    int64_t ntiles, bool lut, int ncols, hipStream_t st, const GTile* gt) {
   const bool pre3 = ncols >= 3;
 #define CALL(KT, U, CZ)                                                                 \
   if (lut && pre3)                                                                      \
     scatter_kernel<KT, U, true, CZ, true><<<(unsigned)ntiles, kScatterThreads, 0, st>>>(  \
-        d, plan, tile_seg, offs, offs32);                                               \
+        d, plan, tile_seg, offs, offs32, gt);                                               \
   else if (lut)                                                                         \
     scatter_kernel<KT, U, true, CZ, false><<<(unsigned)ntiles, kScatterThreads, 0, st>>>( \
-        d, plan, tile_seg, offs, offs32);                                               \
+        d, plan, tile_seg, offs, offs32, gt);                                               \
   else if (pre3)                                                                        \
     scatter_kernel<KT, U, false, CZ, true><<<(unsigned)ntiles, kScatterThreads, 0, st>>>( \
-        d, plan, tile_seg, offs, offs32);                                               \
+        d, plan, tile_seg, offs, offs32, gt);                                               \
   else                                                                                  \
     scatter_kernel<KT, U, false, CZ, false><<<(unsigned)ntiles, kScatterThreads, 0, st>>>( \
-        d, plan, tile_seg, offs, offs32)
+        d, plan, tile_seg, offs, offs32, gt)
   SRS_KEY_DISPATCH(key_size, CALL)
 #undef CALL
+}
+
+void launch_stripe_tables(const uint32_t* prun, int64_t nstripes, int nb, uint32_t* ptile,
+                          uint64_t* btot, uint32_t* bnt, int rbits, int buf, Seg* big,
+                          int32_t* nt_over, uint32_t* btile, ListCounters* ctr,
+                          const uint64_t* sbase, const SegPlan* plan, GTile* gt,
+                          const int32_t* lut_rbits, hipStream_t st) {
+  stripe_tiles_kernel<<<(unsigned)nb, kStripeThreads, 0, st>>>(prun, nstripes, ptile, btot, bnt);
+  stripe_segs_kernel<<<1, kMaxBins, 0, st>>>(btot, bnt, nb, rbits, buf, big, nt_over, btile, ctr,
+                                             lut_rbits);
+  const int64_t np = nstripes * nb;
+  stripe_gtile_kernel<<<(unsigned)((np + 255) / 256), 256, 0, st>>>(prun, ptile, btile, sbase,
+                                                                    plan, nstripes, nb, gt);
 }
 
 void launch_local(int key_size, const SortDesc* d, const Seg* segs, int64_t nsegs, int big_class,

@@ -577,6 +577,105 @@ def test_scale_distributions_vs_torch_stable(dist):
     assert torch.equal(po, ref_i)
 
 
+@pytest.mark.parametrize("case", ["u32_pays_down_inplace", "i64_keys_only", "u64_fewbuckets",
+                                  "u32_equal", "u64_tiny_pieces"])
+def test_stripe_first_level(case):
+    """n >= 2^25 plain SoA sorts take the stripe first level (each stripe
+    partitioned on its own, the second level reading every bucket's pieces
+    through gathered tiles): keys and every payload column against torch's
+    stable sort, including pieces far from their average size (few buckets
+    used, all-equal keys, buckets that most stripes leave nearly empty)."""
+    torch = _torch()
+    n = (1 << 25) + 4099
+    g = torch.Generator(device="cuda")
+    g.manual_seed(17)
+    idx = torch.arange(n, dtype=torch.int64, device="cuda")
+    up = True
+    if case == "u32_pays_down_inplace":
+        keys = torch.randint(-2**31, 2**31 - 1, (n,), dtype=torch.int32, device="cuda", generator=g)
+        kind, up = srs_amd.KEY_U32, False
+    elif case == "i64_keys_only":
+        keys = torch.randint(-2**63, 2**63 - 1, (n,), dtype=torch.int64, device="cuda", generator=g)
+        kind = srs_amd.KEY_I64
+    elif case == "u64_fewbuckets":  # 3 top-digit buckets, uniform below
+        keys = (torch.randint(0, 3, (n,), dtype=torch.int64, device="cuda", generator=g) << 61) | \
+            torch.randint(0, 2**40, (n,), dtype=torch.int64, device="cuda", generator=g)
+        kind = srs_amd.KEY_U64
+    elif case == "u32_equal":
+        keys = torch.full((n,), 77, dtype=torch.int32, device="cuda")
+        kind = srs_amd.KEY_U32
+    else:  # one key in 4096 per top bucket region: most pieces hold 0-2 records
+        keys = torch.randint(0, 2**62, (n,), dtype=torch.int64, device="cuda", generator=g)
+        keys = torch.where(idx % 4096 == 0, keys, keys & 0xFFFFFFFF)
+        kind = srs_amd.KEY_U64
+    if keys.dtype == torch.int32:
+        order_view = keys ^ torch.iinfo(torch.int32).min if kind == srs_amd.KEY_U32 else keys
+    else:
+        order_view = keys ^ torch.iinfo(torch.int64).min if kind == srs_amd.KEY_U64 else keys
+    if not up:
+        order_view = ~order_view
+    ref_v, ref_i = torch.sort(order_view, stable=True)
+    ref_k = keys[ref_i]
+    if case == "u32_pays_down_inplace":
+        p8 = (idx & 0xFF).to(torch.uint8)
+        p16 = (idx & 0x7FFF).to(torch.int16)
+        p64 = idx.clone()
+        k = keys.clone()
+        srs_amd.sort_device(k, p8, p16, p64, key_kind=kind, up=up)
+        assert torch.equal(k, ref_k)
+        assert torch.equal(p64, ref_i)
+        assert torch.equal(p8, (ref_i & 0xFF).to(torch.uint8))
+        assert torch.equal(p16, (ref_i & 0x7FFF).to(torch.int16))
+    elif case == "i64_keys_only":
+        ko = torch.empty_like(keys)
+        srs_amd.sort_device(keys, key_kind=kind, out=(ko,))
+        assert torch.equal(ko, ref_k)
+    else:
+        ko, po = torch.empty_like(keys), torch.empty_like(idx)
+        srs_amd.sort_device(keys, idx, key_kind=kind, out=(ko, po))
+        assert torch.equal(ko, ref_k)
+        assert torch.equal(po, ref_i)
+
+
+@pytest.mark.parametrize("case", ["aos16", "aos32_down", "f32_two_u32_grid", "f32_two_u32_uniform"])
+def test_stripe_first_level_layouts(case):
+    """The stripe first level under the other column layouts: AoS records as
+    slice columns (16 and 32 bytes), C2's key + two 4-byte payloads as word
+    pairs, with the balanced digit-table first level (skewed grid floats) and
+    without it (uniform floats); against torch's stable sort."""
+    torch = _torch()
+    n = (1 << 25) + 777
+    g = torch.Generator(device="cuda")
+    g.manual_seed(23)
+    idx = torch.arange(n, dtype=torch.int64, device="cuda")
+    if case.startswith("aos"):
+        words = 2 if case == "aos16" else 4
+        up = case != "aos32_down"
+        keys = torch.randint(-2**63, 2**63 - 1, (n,), dtype=torch.int64, device="cuda", generator=g)
+        keys = keys >> 40  # duplicates: equal keys must keep input order
+        rec = torch.stack([keys] + [idx * (w + 1) for w in range(words - 1)], dim=1).contiguous()
+        out = torch.empty_like(rec)
+        srs_amd.sort_combined_device(rec, srs_amd.KEY_I64, up=up, out=out)
+        ov = keys if up else ~keys
+        _, ref_i = torch.sort(ov, stable=True)
+        assert torch.equal(out, rec[ref_i])
+        return
+    if case == "f32_two_u32_grid":
+        keys = (torch.randint(0, 1 << 24, (n,), device="cuda", generator=g).to(torch.float32)
+                * (1.0 / (1 << 23)) - 1.0)
+    else:
+        keys = torch.rand(n, device="cuda", generator=g) * 2 - 1
+    keys = torch.where(keys == 0, torch.zeros_like(keys), keys)
+    p0 = idx.to(torch.int32)
+    p1 = (idx * 3).to(torch.int32)
+    ko, o0, o1 = torch.empty_like(keys), torch.empty_like(p0), torch.empty_like(p1)
+    srs_amd.sort_device(keys, p0, p1, key_kind=srs_amd.KEY_F32, out=(ko, o0, o1))
+    ref_k, ref_i = torch.sort(keys, stable=True)
+    assert torch.equal(ko.view(torch.int32), ref_k.view(torch.int32))
+    assert torch.equal(o0, ref_i.to(torch.int32))
+    assert torch.equal(o1, (ref_i * 3).to(torch.int32))
+
+
 def test_more_than_2_pow_32_keys():
     """n > 2^32: positions, tile indices and offsets are 64-bit throughout.
     u32 keys (17 GB), in place; checked by order and by two multiset sums."""
