@@ -655,57 +655,75 @@ __device__ __forceinline__ DigitLut stage_lut(const SortDesc* desc, uint16_t* sl
 // ---------------------------------------------------------------------------
 // count: per-tile digit histogram (one tile-major row per tile) + varying bits
 // ---------------------------------------------------------------------------
-template <typename KT, typename U, bool LUT, bool CZ>
-__global__ __launch_bounds__(kCountThreads) void count_kernel(
-    const SortDesc* __restrict__ desc, const SegPlan* __restrict__ plan,
-    const int32_t* __restrict__ tile_seg, uint16_t* __restrict__ hist,
-    unsigned long long* __restrict__ var_or, const GTile* __restrict__ gt) {
-  __shared__ uint32_t h[kMaxBins];
-  __shared__ unsigned long long sh_or;
-  const int64_t t = xcd_remap(blockIdx.x, gridDim.x);
-  const int32_t s = tile_seg[t];
-  const SegPlan P = plan[s];
-  const int64_t tl = t - P.tile_base;
-  const uint32_t nb = 1u << P.bits;
-  const uint32_t mask = nb - 1;
-  Xform<U, CZ> xf;
-  xf.init(*desc);
+// A workgroup counts kCountTiles consecutive tiles; the next tile's loads go
+// out before the current one is counted (two register sets, LDS-only
+// barriers), so a workgroup's reads stay in flight across its tiles.
+#ifndef SRS_COUNT_TILES
+#define SRS_COUNT_TILES 1
+#endif
+constexpr int kCountTiles = SRS_COUNT_TILES;
+
+struct CountTile {
+  int64_t t;     // tile index (its histogram row)
+  int32_t s;     // segment
+  int32_t cnt;   // keys in the tile (0: none / past the last tile)
+  bool vec;      // dense 4/8-byte keys read in 16-byte pieces
+};
+
+// element of item k: a dense 4/8-byte key column is read in 16-byte pieces
+// (range-checked buffer loads; piece j of thread i holds elements
+// (j * NT + i) * PER ...), anything else (1/2-byte keys, AoS records) one key
+// per load. The histogram does not depend on the mapping.
+template <typename KT>
+__device__ __forceinline__ int count_elem(bool vec, int k) {
+  constexpr int KB = (int)sizeof(KT);
+  constexpr int PER = KB >= 4 ? 16 / KB : 1;
+  return vec ? ((k / PER) * kCountThreads + (int)threadIdx.x) * PER + k % PER
+             : k * kCountThreads + (int)threadIdx.x;
+}
+
+// Issues tile t's key loads (raw) and its segment's reference key (uref_raw).
+template <typename KT, typename U>
+__device__ __forceinline__ CountTile count_load(const SortDesc* __restrict__ desc,
+                                                const SegPlan* __restrict__ plan,
+                                                const int32_t* __restrict__ tile_seg,
+                                                const GTile* __restrict__ gt, int64_t t,
+                                                int64_t ntiles, U (&raw)[kCountItems],
+                                                U& uref_raw) {
+  CountTile T;
+  T.t = t;
+  T.cnt = 0;
+  T.s = 0;
+  T.vec = false;
+  if (t >= ntiles) {
+#pragma unroll
+    for (int k = 0; k < kCountItems; k++) raw[k] = 0;
+    uref_raw = 0;
+    return T;
+  }
+  T.s = tile_seg[t];
+  const SegPlan P = plan[T.s];
   const char* kp = desc->key.base[P.buf];
   const uint32_t ks = desc->key.stride[P.buf];
-  __shared__ alignas(16) uint16_t slut[LUT ? kLdsLutEntries : 8];
-  const DigitLut lut = stage_lut<LUT, kCountThreads>(desc, slut);
-
-  for (uint32_t i = threadIdx.x; i < nb; i += kCountThreads) h[i] = 0;
-  if (threadIdx.x == 0) sh_or = 0;
-  __syncthreads();
-
   int64_t base, first;
-  int cnt;
   if (gt) {  // gathered level: the tile table says where the records are
     base = gt[t].src;
-    cnt = gt[t].cnt;
+    T.cnt = gt[t].cnt;
     first = gt[P.tile_base].src;  // one reference key per segment
   } else {
+    const int64_t tl = t - P.tile_base;
     base = P.start + tl * kTile;
     const int64_t rem = P.len - tl * kTile;
-    cnt = rem < kTile ? (int)rem : kTile;
+    T.cnt = rem < kTile ? (int)rem : kTile;
     first = P.start;
   }
-  const U uref = xf((U)gld<KT>(kp + first * (int64_t)ks));
-  U raw[kCountItems];
-  // element of item k: a dense 4/8-byte key column is read in 16-byte pieces
-  // (range-checked buffer loads; piece j of thread i holds elements
-  // (j * NT + i) * PER ...), anything else (1/2-byte keys, AoS records)
-  // one key per load. The histogram does not depend on the mapping.
+  uref_raw = (U)gld<KT>(kp + first * (int64_t)ks);
   constexpr int KB = (int)sizeof(KT);
   constexpr int PER = KB >= 4 ? 16 / KB : 1;
   static_assert(kCountItems % PER == 0, "whole 16-byte pieces per thread");
-  const bool vec = KB >= 4 && ks == (uint32_t)KB;
-  auto elem = [&](int k) -> int {
-    return vec ? ((k / PER) * kCountThreads + (int)threadIdx.x) * PER + k % PER
-               : k * kCountThreads + (int)threadIdx.x;
-  };
-  if (vec) {
+  T.vec = KB >= 4 && ks == (uint32_t)KB;
+  const int cnt = T.cnt;
+  if (T.vec) {
     typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
     const __amdgpu_buffer_rsrc_t r =
         strip_rsrc(kp + base * (int64_t)KB, cnt > 0 ? (uint32_t)cnt * KB : 0u);
@@ -725,10 +743,27 @@ __global__ __launch_bounds__(kCountThreads) void count_kernel(
   } else {
 #pragma unroll
     for (int k = 0; k < kCountItems; k++) {
-      const int e = elem(k);
+      const int e = count_elem<KT>(false, k);
       raw[k] = e < cnt ? (U)gld<KT>(kp + (base + e) * (int64_t)ks) : (U)0;
     }
   }
+  return T;
+}
+
+// Counts a loaded tile into h (LDS, zeroed) and ORs its varying bits into *sor.
+template <typename KT, typename U, bool LUT, bool CZ>
+__device__ __forceinline__ void count_add(const SortDesc* __restrict__ desc,
+                                          const SegPlan* __restrict__ plan, const CountTile& T,
+                                          const U (&raw)[kCountItems], U uref_raw,
+                                          uint32_t* h, unsigned long long* sor,
+                                          const DigitLut& lut) {
+  if (T.cnt == 0) return;
+  const SegPlan P = plan[T.s];
+  const uint32_t mask = (1u << P.bits) - 1;
+  Xform<U, CZ> xf;
+  xf.init(*desc);
+  const U uref = xf(uref_raw);
+  const int cnt = T.cnt;
   U vor = 0;
   // A wave holds 64 consecutive keys. Sorted or constant inputs give it one
   // digit, and 64 lanes adding into one LDS counter serialise (sorted C1
@@ -739,11 +774,12 @@ __global__ __launch_bounds__(kCountThreads) void count_kernel(
   {
     const uint32_t d = pass_digit<LUT>(xf(raw[0]), P.shift, mask, lut);
     const uint32_t d0 = __builtin_amdgcn_readfirstlane(d);
-    agg = __ballot(elem(0) < cnt && d == d0) == __ballot(elem(0) < cnt);
+    const bool ok0 = count_elem<KT>(T.vec, 0) < cnt;
+    agg = __ballot(ok0 && d == d0) == __ballot(ok0);
   }
 #pragma unroll
   for (int k = 0; k < kCountItems; k++) {
-    const int e = elem(k);
+    const int e = count_elem<KT>(T.vec, k);
     const bool ok = e < cnt;
     const U u = xf(raw[k]);
     const uint32_t d = pass_digit<LUT>(u, P.shift, mask, lut);
@@ -758,19 +794,67 @@ __global__ __launch_bounds__(kCountThreads) void count_kernel(
     }
     if (ok) atomicAdd(&h[d], 1u);
   }
-  if (vor) atomicOr(&sh_or, (unsigned long long)vor);
-  __syncthreads();
-  // tile-major row of u16 counts (a tile holds <= kTile = 4096 keys): one
-  // coalesced 2*nb-byte write per tile, written as packed pairs
+  if (vor) atomicOr(sor, (unsigned long long)vor);
+}
+
+// After a barrier: the tile's row of u16 counts (a tile holds <= kTile = 4096
+// keys; one coalesced 2*nb-byte write, packed pairs), h zeroed again for the
+// tile after next, the varying bits published.
+__device__ __forceinline__ void count_flush(const SegPlan* __restrict__ plan, const CountTile& T,
+                                            uint32_t* h, unsigned long long* sor,
+                                            uint16_t* __restrict__ hist,
+                                            unsigned long long* __restrict__ var_or) {
   static_assert(kTile < 65536, "u16 tile counts");
-  uint32_t* row = (uint32_t*)(hist + t * kMaxBins);
-  for (uint32_t i = threadIdx.x; i < nb / 2; i += kCountThreads)
+  if (T.cnt == 0) return;
+  const uint32_t nb = 1u << plan[T.s].bits;
+  uint32_t* row = (uint32_t*)(hist + T.t * kMaxBins);
+  for (uint32_t i = threadIdx.x; i < nb / 2; i += kCountThreads) {
     row[i] = h[2 * i] | (h[2 * i + 1] << 16);
-  if (threadIdx.x == 0 && sh_or) {
-    // most tiles add no new bits: skip the (contended) atomic then
-    const unsigned long long known =
-        __hip_atomic_load(&var_or[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (sh_or & ~known) atomicOr(&var_or[s], sh_or);
+    h[2 * i] = 0;
+    h[2 * i + 1] = 0;
+  }
+  if (threadIdx.x == 0) {
+    const unsigned long long o = *sor;
+    *sor = 0;
+    if (o) {
+      // most tiles add no new bits: skip the (contended) atomic then
+      const unsigned long long known =
+          __hip_atomic_load(&var_or[T.s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (o & ~known) atomicOr(&var_or[T.s], o);
+    }
+  }
+}
+
+template <typename KT, typename U, bool LUT, bool CZ>
+__global__ __launch_bounds__(kCountThreads) void count_kernel(
+    const SortDesc* __restrict__ desc, const SegPlan* __restrict__ plan,
+    const int32_t* __restrict__ tile_seg, uint16_t* __restrict__ hist,
+    unsigned long long* __restrict__ var_or, const GTile* __restrict__ gt, int64_t ntiles) {
+  constexpr int NH = kCountTiles > 1 ? 2 : 1;  // (one row when nothing is prefetched:
+  __shared__ uint32_t h[NH][kMaxBins];          //  the LUT pass keeps 6 workgroups per CU)
+  __shared__ unsigned long long sh_or[NH];
+  const int64_t t0 = xcd_remap(blockIdx.x, gridDim.x) * kCountTiles;
+  __shared__ alignas(16) uint16_t slut[LUT ? kLdsLutEntries : 8];
+  U ra[kCountItems], rb[kCountItems];
+  U ua, ub;
+  CountTile A = count_load<KT, U>(desc, plan, tile_seg, gt, t0, ntiles, ra, ua);
+  const DigitLut lut = stage_lut<LUT, kCountThreads>(desc, slut);
+  for (uint32_t i = threadIdx.x; i < NH * kMaxBins; i += kCountThreads) (&h[0][0])[i] = 0;
+  if (threadIdx.x < NH) sh_or[threadIdx.x] = 0;
+  lds_barrier();
+#pragma unroll
+  for (int i = 0; i < kCountTiles; i += 2) {
+    CountTile B;
+    if (i + 1 < kCountTiles) B = count_load<KT, U>(desc, plan, tile_seg, gt, t0 + i + 1, ntiles, rb, ub);
+    count_add<KT, U, LUT, CZ>(desc, plan, A, ra, ua, h[0], &sh_or[0], lut);
+    lds_barrier();
+    count_flush(plan, A, h[0], &sh_or[0], hist, var_or);
+    if (i + 1 < kCountTiles) {
+      if (i + 2 < kCountTiles) A = count_load<KT, U>(desc, plan, tile_seg, gt, t0 + i + 2, ntiles, ra, ua);
+      count_add<KT, U, LUT, CZ>(desc, plan, B, rb, ub, h[NH - 1], &sh_or[NH - 1], lut);
+      lds_barrier();
+      count_flush(plan, B, h[NH - 1], &sh_or[NH - 1], hist, var_or);
+    }
   }
 }
 
@@ -2565,13 +2649,14 @@ void launch_seg_map2(const int64_t* tbase, int64_t ntiles, int32_t* tile_seg,
 void launch_count(int key_size, const SortDesc* d, const SegPlan* plan,
                   const int32_t* tile_seg, int64_t ntiles, uint16_t* hist,
                   unsigned long long* var_or, bool lut, hipStream_t st, const GTile* gt) {
+  const unsigned grid = (unsigned)((ntiles + kCountTiles - 1) / kCountTiles);
 #define CALL(KT, U, CZ)                                                                 \
   if (lut)                                                                              \
-    count_kernel<KT, U, true, CZ><<<(unsigned)ntiles, kCountThreads, 0, st>>>(            \
-        d, plan, tile_seg, hist, var_or, gt);                                           \
+    count_kernel<KT, U, true, CZ><<<grid, kCountThreads, 0, st>>>(                       \
+        d, plan, tile_seg, hist, var_or, gt, ntiles);                                   \
   else                                                                                  \
-    count_kernel<KT, U, false, CZ><<<(unsigned)ntiles, kCountThreads, 0, st>>>(           \
-        d, plan, tile_seg, hist, var_or, gt)
+    count_kernel<KT, U, false, CZ><<<grid, kCountThreads, 0, st>>>(                      \
+        d, plan, tile_seg, hist, var_or, gt, ntiles)
   SRS_KEY_DISPATCH(key_size, CALL)
 #undef CALL
 }
