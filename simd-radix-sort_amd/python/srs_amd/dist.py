@@ -6,16 +6,19 @@ Protocol, per rank r holding n_r records (key + payload columns)
   2. all-reduce of the 2^bits histogram                   (RCCL, 32 KB at 12 bits)
   3. bins -> G (<= 512) key-range groups of ~equal size; contiguous runs of
      groups -> ranks, again balanced by size
-  4. stable partition of the local records into the G groups
-                                                          (srs_partition_device)
-     This IS the first MSB level of the sort: nothing is partitioned twice.
-  5. all-gather of the G group sizes of every rank -> receive layout
+  4. all-gather of every rank's group sizes per input chunk (exact from
+     per-chunk histograms: a group is a union of bins) -> receive layout
+  5. stable partition of the local records into the G groups, chunk by
+     chunk (srs_partition_device). This IS the first MSB level of the sort:
+     nothing is partitioned twice. Each chunk's first-round messages go out
+     as soon as it is partitioned, while the next chunk is partitioned.
   6. the groups move peer to peer (batched isend/irecv = RCCL grouped
      send/recv over xGMI) in `rounds`: round i moves a contiguous run of
      each receiver's groups, one message per (round, peer, column), each
      <= 256 MB (RCCL corrupted a single 8 GB all_to_all message: measured at
      world 1, 1e9 int64; 1e8 was exact). A round lands source-major in its
-     own key range of the receive buffer; while round i+1 is in flight,
+     own key range of the receive buffer (source-major, then chunk: input
+     order of equal keys is kept); while round i+1 is in flight,
      round i's range is sorted on a second stream (srs_sort_segments_device)
 Rank r then holds the r-th slice of the globally sorted array: every key on
 rank r orders before every key on rank r+1.
@@ -97,7 +100,7 @@ class ShardSorter:
 
     def __init__(self, ops, n_local: int, payload_dtypes, key_dtype, device, bits: int = 12,
                  groups: int = 512, rounds: int = 4, slack: float = 1.25, group=None,
-                 chunk_bytes: int = 256 << 20, stage_host: bool = False):
+                 chunk_bytes: int = 256 << 20, stage_host: bool = False, chunks: int = 4):
         # stage_host: the messages travel through host memory (test mode:
         # several gloo ranks sharing one GPU run the real kernels; RCCL
         # cannot put two ranks on one device)
@@ -113,6 +116,10 @@ class ShardSorter:
         self.device = device
         self.n = n_local
         self.chunk_bytes = chunk_bytes
+        # input chunks partitioned one after another, each one's first-round
+        # messages overlapping the next one's partition (one at world 1: no
+        # messages, and each group stays one contiguous segment)
+        self.chunks = max(1, chunks) if self.world > 1 else 1
         cap = int(n_local * slack) + 1024
         self.part_keys = torch.empty(n_local, dtype=key_dtype, device=device)
         self.part_pays = [torch.empty(n_local, dtype=dt, device=device) for dt in payload_dtypes]
@@ -152,43 +159,55 @@ class ShardSorter:
             self.part_keys = torch.empty(n, dtype=keys.dtype, device=self.device)
             self.part_pays = [torch.empty(n, dtype=p.dtype, device=self.device)
                               for p in self.part_pays]
-        # 1-3: global histogram -> key-range groups -> ranks
-        hist = self.ops.histogram(keys, self.bits)
+        C = max(1, min(self.chunks, n))
+        cb = [n * c // C for c in range(C + 1)]          # chunk c = input [cb[c], cb[c+1])
+        # 1-3: per-chunk histograms -> global histogram -> groups -> ranks
+        hists = [self.ops.histogram(keys[cb[c]:cb[c + 1]], self.bits) for c in range(C)]
+        hist = hists[0].clone()
+        for h in hists[1:]:
+            hist += h
         dist.all_reduce(hist, group=self.group)
         group_of_bin, rank_of_group, first, last = self.plan(hist)
-        # 4: stable partition into the groups (the first radix level)
-        counts = self.ops.partition(keys, pays, self.bits, group_of_bin, G,
-                                    (self.part_keys, *self.part_pays))
-        # 5: everyone's group sizes -> receive layout
-        send = torch.tensor(counts, dtype=torch.int64, device=hist.device)
-        mat = [torch.empty_like(send) for _ in range(w)]
-        dist.all_gather(mat, send, group=self.group)
-        mat = [m.tolist() for m in mat]                   # mat[src][g]
+        # 4: every rank's group sizes per chunk (a group is a union of bins,
+        # so the chunk histograms give them exactly) -> receive layout; known
+        # before any partition, so no collective waits behind the messages
+        gob = group_of_bin.to(torch.int64)
+        cc = torch.zeros(C, G, dtype=torch.int64, device=hist.device)
+        for c in range(C):
+            cc[c].index_add_(0, gob, hists[c].to(torch.int64))
+        allcc = [torch.empty_like(cc) for _ in range(w)]
+        dist.all_gather(allcc, cc, group=self.group)
+        mat = [m.tolist() for m in allcc]                 # mat[src][chunk][g]
+        counts = [sum(mat[me][c][g] for c in range(C)) for g in range(G)]
         owned = [[g for g in range(G) if rank_of_group[g] == r] for r in range(w)]
         # exchange round r of rank d moves d's groups owned[d][rg[d][r]]: a
         # contiguous run of groups, hence one contiguous piece of every
-        # sender's partitioned buffer
+        # sender's partitioned chunk
         rg = [[range(i * len(owned[d]) // R, (i + 1) * len(owned[d]) // R) for i in range(R)]
               for d in range(w)]
-        soff = [0] * (G + 1)
-        for g in range(G):
-            soff[g + 1] = soff[g] + counts[g]
+        soff = []                                         # soff[c][g]: group g of chunk c
+        for c in range(C):
+            o = [cb[c]] * (G + 1)
+            for g in range(G):
+                o[g + 1] = o[g] + mat[me][c][g]
+            soff.append(o)
 
         def piece(src_counts, d, r):
             """(first group, #records) of the round-r piece for rank d"""
             gs = [owned[d][i] for i in rg[d][r]]
             return (gs[0] if gs else 0), sum(src_counts[g] for g in gs)
 
-        # receive layout: round-major, then source-major (sources in rank
-        # order): one message per (round, peer, column). Equal keys share a
+        # receive layout: round-major, then source (rank order), then chunk:
+        # one message per (round, peer, chunk, column). Equal keys share a
         # group, so inside a round they arrive in (source rank, input index)
         # order, and the round's key range lies above the previous round's.
         roff, rbound, pos = {}, [], 0
         for r in range(R):
             start = pos
             for src in range(w):
-                roff[(r, src)] = pos
-                pos += piece(mat[src], me, r)[1]
+                for c in range(C):
+                    roff[(r, src, c)] = pos
+                    pos += piece(mat[src][c], me, r)[1]
             rbound.append((start, pos))
         total = pos
         self._ensure_capacity(total)
@@ -197,28 +216,31 @@ class ShardSorter:
         cols = [(self.part_keys, rk)] + list(zip(self.part_pays, rps))
         mcols = cols                                      # what the messages move
         if self.stage_host:
-            mcols = [(sb[:n].cpu(), torch.empty(total, dtype=rb.dtype)) for sb, rb in cols]
+            # (host buffers, filled chunk by chunk as they are partitioned)
+            mcols = [(torch.empty(n, dtype=sb.dtype), torch.empty(total, dtype=rb.dtype))
+                     for sb, rb in cols]
 
-        # 6: rounds of peer-to-peer moves; round r+1 is in flight before the
-        # (host-synchronising) sort of round r is queued
-        def issue(r):
+        # 6: rounds of peer-to-peer moves for the given chunks; round r+1 is in
+        # flight before the (host-synchronising) sort of round r is queued
+        def issue(r, chunks):
             p2p = []
             for d in range(w):
-                g0, cnt = piece(counts, d, r)
-                if d == me:
-                    for src in range(w):
-                        rcnt = piece(mat[src], me, r)[1]
-                        if rcnt == 0:
-                            continue
-                        a = roff[(r, src)]
-                        for (sbuf, rbuf), (_, mrbuf) in zip(cols, mcols):
-                            if src == me:
-                                rbuf[a:a + rcnt].copy_(sbuf[soff[g0]:soff[g0] + rcnt])
-                            else:
-                                self._msgs(p2p, dist.irecv, mrbuf, a, rcnt, src)
-                elif cnt:
-                    for msbuf, _ in mcols:
-                        self._msgs(p2p, dist.isend, msbuf, soff[g0], cnt, d)
+                for c in chunks:
+                    g0, cnt = piece(mat[me][c], d, r)
+                    if d == me:
+                        for src in range(w):
+                            rcnt = piece(mat[src][c], me, r)[1]
+                            if rcnt == 0:
+                                continue
+                            a = roff[(r, src, c)]
+                            for (sbuf, rbuf), (_, mrbuf) in zip(cols, mcols):
+                                if src == me:
+                                    rbuf[a:a + rcnt].copy_(sbuf[soff[c][g0]:soff[c][g0] + rcnt])
+                                else:
+                                    self._msgs(p2p, dist.irecv, mrbuf, a, rcnt, src)
+                    elif cnt:
+                        for msbuf, _ in mcols:
+                            self._msgs(p2p, dist.isend, msbuf, soff[c][g0], cnt, d)
             return dist.batch_isend_irecv(p2p) if p2p else []
 
         def land(r):
@@ -226,16 +248,29 @@ class ShardSorter:
             for src in range(w):
                 if src == me:
                     continue
-                a, rcnt = roff[(r, src)], piece(mat[src], me, r)[1]
-                if rcnt:
-                    for (_, rbuf), (_, mrbuf) in zip(cols, mcols):
-                        rbuf[a:a + rcnt].copy_(mrbuf[a:a + rcnt])
+                for c in range(C):
+                    a, rcnt = roff[(r, src, c)], piece(mat[src][c], me, r)[1]
+                    if rcnt:
+                        for (_, rbuf), (_, mrbuf) in zip(cols, mcols):
+                            rbuf[a:a + rcnt].copy_(mrbuf[a:a + rcnt])
 
-        pending = issue(0)
+        # 5: partition chunk by chunk; each chunk's round-0 messages go out
+        # while the next chunk is partitioned
+        pending = []
+        for c in range(C):
+            a, b = cb[c], cb[c + 1]
+            got = self.ops.partition(keys[a:b], [p[a:b] for p in pays], self.bits, group_of_bin,
+                                     G, (self.part_keys[a:b], *[p[a:b] for p in self.part_pays]))
+            if list(got) != mat[me][c]:
+                raise RuntimeError("partition sizes differ from the chunk histogram")
+            if self.stage_host:  # the staged send buffers take the partitioned chunk
+                for (sb, _), (msb, _) in zip(cols, mcols):
+                    msb[a:b].copy_(sb[a:b])
+            pending += issue(0, [c])
         for r in range(R):
             for req in pending:
                 req.wait()
-            pending = issue(r + 1) if r + 1 < R else []
+            pending = issue(r + 1, range(C)) if r + 1 < R else []
             if self.stage_host:
                 land(r)
             a, b = rbound[r]
@@ -248,7 +283,7 @@ class ShardSorter:
                         return 0
                     lo, hi = bins[0][0], bins[-1][1]
                     return min(self.bits - (lo ^ hi).bit_length(), self.key_bits - 1)
-                if w == 1:
+                if w == 1 and C == 1:
                     # one source: the round's groups lie contiguous, each its
                     # own segment (the partition was their first level)
                     bounds = [a]
@@ -256,12 +291,13 @@ class ShardSorter:
                         bounds.append(bounds[-1] + counts[g])
                     self.ops.sort_segments(rk, rps, bounds, min(shared([g]) for g in gs))
                 else:
-                    # several sources interleave the groups: the round's key
-                    # range is one segment (at w >= 2 its size needs no more
-                    # levels than a group's would)
+                    # several sources (or chunks) interleave the groups: the
+                    # round's key range is one segment (at w >= 2 its size
+                    # needs no more levels than a group's would)
                     self.ops.sort_segments(rk, rps, [a, b], shared(gs))
         self.ops.finish(self.device)
-        self.last_counts = (counts, [sum(mat[s][g] for g in owned[me]) for s in range(w)])
+        self.last_counts = (counts, [sum(mat[s][c][g] for c in range(C) for g in owned[me])
+                                     for s in range(w)])
         return rk, rps
 
     def _msgs(self, p2p, op, buf, off, cnt, peer):

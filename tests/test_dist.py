@@ -64,7 +64,7 @@ class NumpyShardOps:
         pass
 
 
-def _worker(rank, world, port, kind, n_per, dist_kind, q, bits=8):
+def _worker(rank, world, port, kind, n_per, dist_kind, q, bits=8, chunks=4):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "simd-radix-sort_amd",
@@ -72,7 +72,7 @@ def _worker(rank, world, port, kind, n_per, dist_kind, q, bits=8):
     from srs_amd.dist import ShardSorter
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        _run(rank, world, kind, n_per, dist_kind, q, bits)
+        _run(rank, world, kind, n_per, dist_kind, q, bits, chunks)
     except Exception as e:  # report instead of hanging the parent
         q.put(("error", repr(e)))
         raise
@@ -80,7 +80,7 @@ def _worker(rank, world, port, kind, n_per, dist_kind, q, bits=8):
         dist.destroy_process_group()
 
 
-def _run(rank, world, kind, n_per, dist_kind, q, bits=8):
+def _run(rank, world, kind, n_per, dist_kind, q, bits=8, chunks=4):
     from srs_amd.dist import ShardSorter
     if True:
         rng = np.random.default_rng(100 + rank)
@@ -96,7 +96,7 @@ def _run(rank, world, kind, n_per, dist_kind, q, bits=8):
         keys = torch.from_numpy(k.copy())
         pay = torch.from_numpy(np.arange(n, dtype=np.int64) + rank * 10**9)
         sorter = ShardSorter(NumpyShardOps(kind), n, [torch.int64], keys.dtype, "cpu", bits=bits,
-                             chunk_bytes=1024)  # many exchange rounds
+                             chunk_bytes=1024, chunks=chunks)  # many exchange rounds
         # never more groups than histogram bins of the (clamped) key width
         assert sorter.groups <= 1 << sorter.bits
         ok, (op,) = sorter.sort(keys, [pay])
@@ -128,11 +128,12 @@ def _run(rank, world, kind, n_per, dist_kind, q, bits=8):
             q.put((sorted_ok, True, True, None))
 
 
-def _run_world(world, kind, dist_kind, bits=8):
+def _run_world(world, kind, dist_kind, bits=8, chunks=4):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, kind, 3000, dist_kind, q, bits))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, kind, 3000, dist_kind, q, bits,
+                                               chunks))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -153,6 +154,13 @@ def _run_world(world, kind, dist_kind, bits=8):
 @pytest.mark.parametrize("dist_kind", ["uniform", "skewed", "equal"])
 def test_shard_sort_gloo(world, dist_kind):
     _run_world(world, 6, dist_kind)
+
+
+@pytest.mark.parametrize("chunks", [1, 3])
+def test_shard_sort_gloo_partition_chunks(chunks):
+    """the partition in 1 or 3 input chunks (the first round's messages of a
+    chunk overlap the next chunk's partition): same result, stable"""
+    _run_world(3, 6, "skewed", chunks=chunks)
 
 
 @pytest.mark.parametrize("kind", [0, 3])  # u8, i16: keys narrower than the default 12 bits
