@@ -142,7 +142,10 @@ constexpr int kTile = kScatterThreads * kScatterItems;   // keys per tile
 constexpr int kCountThreads = SRS_COUNT_THREADS;         // count kernel: one tile per block
 constexpr int kCountItems = kTile / kCountThreads;
 static_assert(kCountItems * kCountThreads == kTile, "count block shape");
-constexpr int kMaxDigitBits = 9;
+#ifndef SRS_MAX_DIGIT_BITS
+#define SRS_MAX_DIGIT_BITS 9
+#endif
+constexpr int kMaxDigitBits = SRS_MAX_DIGIT_BITS;
 // launch_* key_size flag: the canon-zero float case (SortDesc::canon_zero),
 // selects the kernel instantiations that map -0.0 to +0.0
 #define SRS_KS_CANON 0x100
