@@ -637,7 +637,8 @@ def test_stripe_first_level(case):
         assert torch.equal(po, ref_i)
 
 
-@pytest.mark.parametrize("case", ["aos16", "aos32_down", "f32_two_u32_grid", "f32_two_u32_uniform"])
+@pytest.mark.parametrize("case", ["aos16", "aos32_down", "aos16_inplace", "aos8",
+                                  "f32_two_u32_grid", "f32_two_u32_uniform", "u64_six_payloads"])
 def test_stripe_first_level_layouts(case):
     """The stripe first level under the other column layouts: AoS records as
     slice columns (16 and 32 bytes), C2's key + two 4-byte payloads as word
@@ -648,17 +649,44 @@ def test_stripe_first_level_layouts(case):
     g = torch.Generator(device="cuda")
     g.manual_seed(23)
     idx = torch.arange(n, dtype=torch.int64, device="cuda")
+    if case == "aos8":  # DataElement<int32, int32>: one 8-byte column
+        keys = torch.randint(-2**31, 2**31 - 1, (n,), dtype=torch.int32, device="cuda",
+                             generator=g) >> 8
+        rec = torch.stack([keys, idx.to(torch.int32)], dim=1).contiguous()
+        out = torch.empty_like(rec)
+        srs_amd.sort_combined_device(rec, srs_amd.KEY_I32, out=out)
+        _, ref_i = torch.sort(keys, stable=True)
+        assert torch.equal(out, rec[ref_i])
+        return
     if case.startswith("aos"):
-        words = 2 if case == "aos16" else 4
+        words = 4 if case == "aos32_down" else 2
         up = case != "aos32_down"
         keys = torch.randint(-2**63, 2**63 - 1, (n,), dtype=torch.int64, device="cuda", generator=g)
         keys = keys >> 40  # duplicates: equal keys must keep input order
         rec = torch.stack([keys] + [idx * (w + 1) for w in range(words - 1)], dim=1).contiguous()
-        out = torch.empty_like(rec)
-        srs_amd.sort_combined_device(rec, srs_amd.KEY_I64, up=up, out=out)
         ov = keys if up else ~keys
         _, ref_i = torch.sort(ov, stable=True)
-        assert torch.equal(out, rec[ref_i])
+        exp = rec[ref_i]
+        if case == "aos16_inplace":
+            srs_amd.sort_combined_device(rec, srs_amd.KEY_I64, up=up)
+            assert torch.equal(rec, exp)
+        else:
+            out = torch.empty_like(rec)
+            srs_amd.sort_combined_device(rec, srs_amd.KEY_I64, up=up, out=out)
+            assert torch.equal(out, exp)
+        return
+    if case == "u64_six_payloads":
+        keys = torch.randint(-2**63, 2**63 - 1, (n,), dtype=torch.int64, device="cuda", generator=g)
+        pays = [(idx * (c + 1)).to(dt) for c, dt in
+                enumerate([torch.int64, torch.int32, torch.int16, torch.uint8, torch.int64,
+                           torch.int32])]
+        outs = [torch.empty_like(p) for p in pays]
+        ko = torch.empty_like(keys)
+        srs_amd.sort_device(keys, *pays, key_kind=srs_amd.KEY_U64, out=(ko, *outs))
+        _, ref_i = torch.sort(keys ^ torch.iinfo(torch.int64).min, stable=True)
+        assert torch.equal(ko, keys[ref_i])
+        for p, o in zip(pays, outs):
+            assert torch.equal(o, p[ref_i])
         return
     if case == "f32_two_u32_grid":
         keys = (torch.randint(0, 1 << 24, (n,), device="cuda", generator=g).to(torch.float32)
