@@ -5,6 +5,8 @@ radixRecursion + CmpSorterInsertionSort. It is pinned here against golden
 vectors produced by the reference itself (tests/golden/, oracle/gen_golden.cpp)
 and, where this host can run AVX-512 VBMI2, against the reference's own sort
 built from /root/reference (oracle/_ref/libsrs_ref.so)."""
+import os
+
 import numpy as np
 import pytest
 
@@ -106,3 +108,19 @@ def test_oracle_vs_reference_combined(esz):
     oracle_sort_aos(4, True, a)
     ref_sort_aos(4, True, b)
     assert beq(a, b)
+
+
+def test_oracle_under_address_and_ub_sanitizers():
+    """The C restatement built with -fsanitize=address,undefined (oracle/Makefile
+    `asan`) sorts every key kind, both directions, SoA payload
+    packs and AoS records of 2-64 bytes around the leaf threshold and the
+    emulated vector widths; the reference's invariants must hold and no
+    sanitizer may fire."""
+    import subprocess
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    subprocess.run(["make", "-C", os.path.join(repo, "oracle"), "asan"], check=True,
+                   capture_output=True)
+    r = subprocess.run([os.path.join(repo, "oracle", "_build", "asan_check")],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "0 failures" in r.stdout and "ERROR" not in r.stderr
