@@ -597,16 +597,16 @@ def test_stripe_first_level(case):
     elif case == "i64_keys_only":
         keys = torch.randint(-2**63, 2**63 - 1, (n,), dtype=torch.int64, device="cuda", generator=g)
         kind = srs_amd.KEY_I64
-    elif case == "u64_fewbuckets":  # 3 top-digit buckets, uniform below
-        keys = (torch.randint(0, 3, (n,), dtype=torch.int64, device="cuda", generator=g) << 61) | \
+    elif case == "u64_fewbuckets":  # every other top-digit bucket empty, uniform below
+        keys = (torch.randint(0, 256, (n,), dtype=torch.int64, device="cuda", generator=g) << 56) | \
             torch.randint(0, 2**40, (n,), dtype=torch.int64, device="cuda", generator=g)
         kind = srs_amd.KEY_U64
-    elif case == "u32_equal":
+    elif case == "u32_equal":  # the key sample declines the stripe level: plain path
         keys = torch.full((n,), 77, dtype=torch.int32, device="cuda")
         kind = srs_amd.KEY_U32
-    else:  # one key in 4096 per top bucket region: most pieces hold 0-2 records
-        keys = torch.randint(0, 2**62, (n,), dtype=torch.int64, device="cuda", generator=g)
-        keys = torch.where(idx % 4096 == 0, keys, keys & 0xFFFFFFFF)
+    else:  # sorted keys: a stripe holds one or two buckets, every other piece is empty
+        keys = torch.sort(torch.randint(0, 2**62, (n,), dtype=torch.int64, device="cuda",
+                                        generator=g))[0]
         kind = srs_amd.KEY_U64
     if keys.dtype == torch.int32:
         order_view = keys ^ torch.iinfo(torch.int32).min if kind == srs_amd.KEY_U32 else keys
