@@ -1322,7 +1322,8 @@ int srs_release_workspace(void) {
     DevBuf* bufs[] = {&w->tmp, &w->tmp2, &w->stage, &w->desc, &w->big[0], &w->big[1], &w->local, &w->local2, &w->fallback, &w->fallback2, &w->shist, &w->lut, &w->lut_rbits,
                       &w->copy, &w->plan, &w->tcount, &w->gcount, &w->tbase, &w->gbase,
                       &w->var, &w->sbase, &w->tile_seg, &w->group_seg, &w->hist, &w->offs,
-                      &w->gsum, &w->gofs, &w->scan_tmp, &w->totals, &w->ctr, &w->small_taken};
+                      &w->gsum, &w->gofs, &w->scan_tmp, &w->totals, &w->ctr, &w->small_taken,
+                      &w->prun, &w->ptile, &w->btot, &w->bnt, &w->btile, &w->nt_over, &w->gtile};
     for (DevBuf* b : bufs)
       if (b->p) (void)hipFree(b->p);
     (void)hipHostFree(w->h_ctr);

@@ -630,6 +630,11 @@ def test_stripe_first_level(case):
         ko = torch.empty_like(keys)
         srs_amd.sort_device(keys, key_kind=kind, out=(ko,))
         assert torch.equal(ko, ref_k)
+        # the workspace (stripe tables included) is freed and grown again
+        srs_amd.release_workspace()
+        ko.zero_()
+        srs_amd.sort_device(keys, key_kind=kind, out=(ko,))
+        assert torch.equal(ko, ref_k)
     else:
         ko, po = torch.empty_like(keys), torch.empty_like(idx)
         srs_amd.sort_device(keys, idx, key_kind=kind, out=(ko, po))
