@@ -642,6 +642,38 @@ def test_stripe_first_level(case):
         assert torch.equal(po, ref_i)
 
 
+@pytest.mark.parametrize("kind", ["u32", "i32", "f32", "u64", "i64", "f64"])
+@pytest.mark.parametrize("up", [True, False])
+def test_stripe_first_level_key_kinds(kind, up):
+    """Every 4- and 8-byte key kind, both directions, through the stripe first
+    level (uniform keys: the key sample lets it run; floats in [-1e6, 1e6),
+    no -0.0 or NaN), with the input index as payload: keys and payloads equal
+    torch's stable sort in the reference's order."""
+    torch = _torch()
+    n = (1 << 25) + 1234
+    g = torch.Generator(device="cuda")
+    g.manual_seed(29)
+    idx = torch.arange(n, dtype=torch.int64, device="cuda")
+    if kind in ("u32", "i32"):
+        keys = torch.randint(-2**31, 2**31 - 1, (n,), dtype=torch.int32, device="cuda", generator=g)
+        ov = keys ^ torch.iinfo(torch.int32).min if kind == "u32" else keys
+    elif kind in ("u64", "i64"):
+        keys = torch.randint(-2**63, 2**63 - 1, (n,), dtype=torch.int64, device="cuda", generator=g)
+        ov = keys ^ torch.iinfo(torch.int64).min if kind == "u64" else keys
+    else:
+        dt = torch.float32 if kind == "f32" else torch.float64
+        keys = (torch.rand(n, device="cuda", generator=g, dtype=dt) * 2 - 1) * 1e6
+        keys = torch.where(keys == 0, torch.ones_like(keys), keys)
+        ov = keys
+    ref_v, ref_i = torch.sort(ov if up else (-ov if kind in ("f32", "f64") else ~ov), stable=True)
+    kk = {"u32": srs_amd.KEY_U32, "i32": srs_amd.KEY_I32, "f32": srs_amd.KEY_F32,
+          "u64": srs_amd.KEY_U64, "i64": srs_amd.KEY_I64, "f64": srs_amd.KEY_F64}[kind]
+    ko, po = torch.empty_like(keys), torch.empty_like(idx)
+    srs_amd.sort_device(keys, idx, key_kind=kk, up=up, out=(ko, po))
+    assert torch.equal(po, ref_i)
+    assert torch.equal(ko, keys[ref_i])
+
+
 @pytest.mark.parametrize("case", ["aos16", "aos32_down", "aos16_inplace", "aos8",
                                   "f32_two_u32_grid", "f32_two_u32_uniform", "u64_six_payloads"])
 def test_stripe_first_level_layouts(case):
