@@ -200,7 +200,7 @@ struct Workspace {
   DevBuf shist, lut, lut_rbits;  // balanced first level (sampled histogram, digit table)
   // stripe first level: piece sizes and tile prefixes, bucket totals, the
   // second level's tile counts and gathered tile table (GTile)
-  DevBuf prun, ptile, btot, bnt, btile, nt_over, gtile;
+  DevBuf prun, ptile, btot, bnt, btile, nt_over, gtile, gorder;
   ListCounters* h_ctr = nullptr;
   uint64_t* h_totals = nullptr;
   // Stream order of the workspace: the last call's kernels may still be
@@ -426,6 +426,7 @@ struct LevelMode {
   int mode = 0;
   const GTile* gt = nullptr;        // mode 2
   const int32_t* nt_over = nullptr; // mode 2: tiles per segment
+  const int32_t* torder = nullptr;  // mode 2: the count's tile order (stripe-major)
   int key_bits = 0;                 // mode 1
 };
 
@@ -499,7 +500,8 @@ int run_level(Workspace* W, int ks, const SortDesc* d_desc, LevelState& S, int f
                   group_seg, nbig, st);
   {
     TimedScope ts("count", (double)0, st);
-    launch_count(ks, d_desc, plan, tile_seg, ntiles, (uint16_t*)W->hist.p, var, lut, st, M.gt);
+    launch_count(ks, d_desc, plan, tile_seg, ntiles, (uint16_t*)W->hist.p, var, lut, st, M.gt,
+                 M.torder);
   }
   // ---- offsets + children (list capacity for the worst case: every bin non-empty)
   const size_t worst = (size_t)nbig * kMaxBins;
@@ -536,7 +538,7 @@ int run_level(Workspace* W, int ks, const SortDesc* d_desc, LevelState& S, int f
                          (uint64_t*)W->btot.p, (uint32_t*)W->bnt.p, rbits, BUF_TMP,
                          (Seg*)W->big[nxt].p, (int32_t*)W->nt_over.p, (uint32_t*)W->btile.p,
                          d_ctr, (const uint64_t*)W->sbase.p, plan, (GTile*)W->gtile.p,
-                         lut_rbits, st);
+                         lut_rbits, st, (int32_t*)W->gorder.p);
   }
   HIP_TRY(hipMemcpyAsync(W->h_ctr, d_ctr, sizeof(ListCounters), hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
@@ -802,6 +804,7 @@ int run_sort(Workspace* W, const Request& R, hipStream_t st) {
     SRS_TRY(ensure(W->nt_over, kMaxBins * 4));
     // tiles of the gathered level: at most one partial tile per piece
     SRS_TRY(ensure(W->gtile, ((n + kTile - 1) / kTile + (size_t)K * nb) * sizeof(GTile)));
+    SRS_TRY(ensure(W->gorder, ((n + kTile - 1) / kTile + (size_t)K * nb) * sizeof(int32_t)));
     HIP_TRY(hipStreamSynchronize(st));  // hs goes out of scope
     S.nbig = K;
     S.known_len = -1;
@@ -818,6 +821,7 @@ int run_sort(Workspace* W, const Request& R, hipStream_t st) {
     m2.mode = 2;
     m2.gt = (const GTile*)W->gtile.p;
     m2.nt_over = (const int32_t*)W->nt_over.p;
+    m2.torder = (const int32_t*)W->gorder.p;
     ++level;
     if (S.nbig > 0) SRS_TRY(run_level(W, ksl, d_desc, S, 0, false, st, nullptr, m2));
   }
@@ -1323,7 +1327,8 @@ int srs_release_workspace(void) {
                       &w->copy, &w->plan, &w->tcount, &w->gcount, &w->tbase, &w->gbase,
                       &w->var, &w->sbase, &w->tile_seg, &w->group_seg, &w->hist, &w->offs,
                       &w->gsum, &w->gofs, &w->scan_tmp, &w->totals, &w->ctr, &w->small_taken,
-                      &w->prun, &w->ptile, &w->btot, &w->bnt, &w->btile, &w->nt_over, &w->gtile};
+                      &w->prun, &w->ptile, &w->btot, &w->bnt, &w->btile, &w->nt_over, &w->gtile,
+                      &w->gorder};
     for (DevBuf* b : bufs)
       if (b->p) (void)hipFree(b->p);
     (void)hipHostFree(w->h_ctr);

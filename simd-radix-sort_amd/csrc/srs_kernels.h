@@ -26,7 +26,7 @@ void launch_plan_bases(SegPlan* plan, int64_t nbig, const int64_t* tbase,
 void launch_count(int key_size, const SortDesc* d, const SegPlan* plan,
                   const int32_t* tile_seg, int64_t ntiles, uint16_t* hist,
                   unsigned long long* var_or, bool lut, hipStream_t st,
-                  const GTile* gt = nullptr);
+                  const GTile* gt = nullptr, const int32_t* torder = nullptr);
 int64_t scan_temp_elems(int64_t n);
 void launch_excl_scan(const uint64_t* x, uint64_t* y, int64_t n, uint64_t* temp,
                       uint64_t* total, hipStream_t st);
@@ -46,7 +46,7 @@ void launch_stripe_tables(const uint32_t* prun, int64_t nstripes, int nb, uint32
                           uint64_t* btot, uint32_t* bnt, int rbits, int buf, Seg* big,
                           int32_t* nt_over, uint32_t* btile, ListCounters* ctr,
                           const uint64_t* sbase, const SegPlan* plan, GTile* gt,
-                          const int32_t* lut_rbits, hipStream_t st);
+                          const int32_t* lut_rbits, hipStream_t st, int32_t* torder = nullptr);
 void launch_key_hist(int key_size, int64_t n, const void* keys, const SortDesc& d, int bits,
                      unsigned long long* hist, hipStream_t st);
 void launch_local(int key_size, const SortDesc* d, const Seg* segs, int64_t nsegs, int big_class,

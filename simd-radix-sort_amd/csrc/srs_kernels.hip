@@ -829,11 +829,15 @@ template <typename KT, typename U, bool LUT, bool CZ>
 __global__ __launch_bounds__(kCountThreads) void count_kernel(
     const SortDesc* __restrict__ desc, const SegPlan* __restrict__ plan,
     const int32_t* __restrict__ tile_seg, uint16_t* __restrict__ hist,
-    unsigned long long* __restrict__ var_or, const GTile* __restrict__ gt, int64_t ntiles) {
+    unsigned long long* __restrict__ var_or, const GTile* __restrict__ gt, int64_t ntiles,
+    const int32_t* __restrict__ torder) {
   constexpr int NH = kCountTiles > 1 ? 2 : 1;  // (one row when nothing is prefetched:
   __shared__ uint32_t h[NH][kMaxBins];          //  the LUT pass keeps 6 workgroups per CU)
   __shared__ unsigned long long sh_or[NH];
-  const int64_t t0 = xcd_remap(blockIdx.x, gridDim.x) * kCountTiles;
+  int64_t t0 = xcd_remap(blockIdx.x, gridDim.x) * kCountTiles;
+  // gathered level: tiles in stripe order (each stripe's pieces lie back to
+  // back, so the reads sweep memory); the rows do not depend on the order
+  if (torder && kCountTiles == 1) t0 = torder[t0];
   __shared__ alignas(16) uint16_t slut[LUT ? kLdsLutEntries : 8];
   U ra[kCountItems], rb[kCountItems];
   U ua, ub;
@@ -1182,6 +1186,31 @@ __global__ __launch_bounds__(kMaxBins) void stripe_segs_kernel(
     nt_over[idx] = (int32_t)nt;
   }
   if (b == 0) ctr->n_big = tot_used;
+}
+
+// The gathered level's tiles in stripe-major order (stripe s's pieces of
+// buckets 0, 1, ... lie back to back in memory): one block; thread = stripe;
+// its row of tiles, a scan over stripes, then each tile's index.
+__global__ __launch_bounds__(1024) void stripe_order_kernel(
+    const uint32_t* __restrict__ prun, const uint32_t* __restrict__ ptile,
+    const uint32_t* __restrict__ btile, int64_t nstripes, int nb, int32_t* __restrict__ torder) {
+  __shared__ uint64_t sh[1024 / 64 + 1];
+  uint64_t carry = 0;
+  for (int64_t s0 = 0; s0 < nstripes; s0 += 1024) {
+    const int64_t s = s0 + threadIdx.x;
+    uint64_t row = 0;
+    if (s < nstripes)
+      for (int b = 0; b < nb; b++) row += (prun[s * kMaxBins + b] + kTile - 1) / kTile;
+    uint64_t tot;
+    uint64_t pos = carry + block_excl_scan<1024>(row, sh, &tot);
+    if (s < nstripes)
+      for (int b = 0; b < nb; b++) {
+        const uint32_t len = prun[s * kMaxBins + b];
+        const uint32_t t = btile[b] + ptile[s * kMaxBins + b];
+        for (uint32_t c = 0; c * (uint32_t)kTile < len; c++) torder[pos++] = (int32_t)(t + c);
+      }
+    carry += tot;
+  }
 }
 
 // One thread per piece: its tiles' table entries (bucket-major, then stripe
@@ -2648,15 +2677,16 @@ void launch_seg_map2(const int64_t* tbase, int64_t ntiles, int32_t* tile_seg,
 
 void launch_count(int key_size, const SortDesc* d, const SegPlan* plan,
                   const int32_t* tile_seg, int64_t ntiles, uint16_t* hist,
-                  unsigned long long* var_or, bool lut, hipStream_t st, const GTile* gt) {
+                  unsigned long long* var_or, bool lut, hipStream_t st, const GTile* gt,
+                  const int32_t* torder) {
   const unsigned grid = (unsigned)((ntiles + kCountTiles - 1) / kCountTiles);
 #define CALL(KT, U, CZ)                                                                 \
   if (lut)                                                                              \
     count_kernel<KT, U, true, CZ><<<grid, kCountThreads, 0, st>>>(                       \
-        d, plan, tile_seg, hist, var_or, gt, ntiles);                                   \
+        d, plan, tile_seg, hist, var_or, gt, ntiles, torder);                           \
   else                                                                                  \
     count_kernel<KT, U, false, CZ><<<grid, kCountThreads, 0, st>>>(                      \
-        d, plan, tile_seg, hist, var_or, gt, ntiles)
+        d, plan, tile_seg, hist, var_or, gt, ntiles, torder)
   SRS_KEY_DISPATCH(key_size, CALL)
 #undef CALL
 }
@@ -2710,13 +2740,14 @@ void launch_stripe_tables(const uint32_t* prun, int64_t nstripes, int nb, uint32
                           uint64_t* btot, uint32_t* bnt, int rbits, int buf, Seg* big,
                           int32_t* nt_over, uint32_t* btile, ListCounters* ctr,
                           const uint64_t* sbase, const SegPlan* plan, GTile* gt,
-                          const int32_t* lut_rbits, hipStream_t st) {
+                          const int32_t* lut_rbits, hipStream_t st, int32_t* torder) {
   stripe_tiles_kernel<<<(unsigned)nb, kStripeThreads, 0, st>>>(prun, nstripes, ptile, btot, bnt);
   stripe_segs_kernel<<<1, kMaxBins, 0, st>>>(btot, bnt, nb, rbits, buf, big, nt_over, btile, ctr,
                                              lut_rbits);
   const int64_t np = nstripes * nb;
   stripe_gtile_kernel<<<(unsigned)((np + 255) / 256), 256, 0, st>>>(prun, ptile, btile, sbase,
                                                                     plan, nstripes, nb, gt);
+  if (torder) stripe_order_kernel<<<1, 1024, 0, st>>>(prun, ptile, btile, nstripes, nb, torder);
 }
 
 void launch_local(int key_size, const SortDesc* d, const Seg* segs, int64_t nsegs, int big_class,
