@@ -201,6 +201,7 @@ struct Workspace {
   // stripe first level: piece sizes and tile prefixes, bucket totals, the
   // second level's tile counts and gathered tile table (GTile)
   DevBuf prun, ptile, btot, bnt, btile, nt_over, gtile, gorder;
+  int64_t gorder_cap = 0;
   ListCounters* h_ctr = nullptr;
   uint64_t* h_totals = nullptr;
   // Stream order of the workspace: the last call's kernels may still be
@@ -538,7 +539,7 @@ int run_level(Workspace* W, int ks, const SortDesc* d_desc, LevelState& S, int f
                          (uint64_t*)W->btot.p, (uint32_t*)W->bnt.p, rbits, BUF_TMP,
                          (Seg*)W->big[nxt].p, (int32_t*)W->nt_over.p, (uint32_t*)W->btile.p,
                          d_ctr, (const uint64_t*)W->sbase.p, plan, (GTile*)W->gtile.p,
-                         lut_rbits, st, (int32_t*)W->gorder.p);
+                         lut_rbits, st, (int32_t*)W->gorder.p, W->gorder_cap);
   }
   HIP_TRY(hipMemcpyAsync(W->h_ctr, d_ctr, sizeof(ListCounters), hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
@@ -804,7 +805,8 @@ int run_sort(Workspace* W, const Request& R, hipStream_t st) {
     SRS_TRY(ensure(W->nt_over, kMaxBins * 4));
     // tiles of the gathered level: at most one partial tile per piece
     SRS_TRY(ensure(W->gtile, ((n + kTile - 1) / kTile + (size_t)K * nb) * sizeof(GTile)));
-    SRS_TRY(ensure(W->gorder, ((n + kTile - 1) / kTile + (size_t)K * nb) * sizeof(int32_t)));
+    W->gorder_cap = (n + kTile - 1) / kTile + (int64_t)K * nb;  // + K entries of scratch
+    SRS_TRY(ensure(W->gorder, (W->gorder_cap + K) * sizeof(int32_t)));
     HIP_TRY(hipStreamSynchronize(st));  // hs goes out of scope
     S.nbig = K;
     S.known_len = -1;

@@ -46,7 +46,8 @@ void launch_stripe_tables(const uint32_t* prun, int64_t nstripes, int nb, uint32
                           uint64_t* btot, uint32_t* bnt, int rbits, int buf, Seg* big,
                           int32_t* nt_over, uint32_t* btile, ListCounters* ctr,
                           const uint64_t* sbase, const SegPlan* plan, GTile* gt,
-                          const int32_t* lut_rbits, hipStream_t st, int32_t* torder = nullptr);
+                          const int32_t* lut_rbits, hipStream_t st, int32_t* torder = nullptr,
+                          int64_t tiles_cap = 0);  // torder: tiles_cap entries + nstripes of scratch
 void launch_key_hist(int key_size, int64_t n, const void* keys, const SortDesc& d, int bits,
                      unsigned long long* hist, hipStream_t st);
 void launch_local(int key_size, const SortDesc* d, const Seg* segs, int64_t nsegs, int big_class,

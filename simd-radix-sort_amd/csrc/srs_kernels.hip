@@ -1189,27 +1189,39 @@ __global__ __launch_bounds__(kMaxBins) void stripe_segs_kernel(
 }
 
 // The gathered level's tiles in stripe-major order (stripe s's pieces of
-// buckets 0, 1, ... lie back to back in memory): one block; thread = stripe;
-// its row of tiles, a scan over stripes, then each tile's index.
-__global__ __launch_bounds__(1024) void stripe_order_kernel(
+// buckets 0, 1, ... lie back to back in memory), for its count. Block per
+// stripe, thread per bucket: the stripe's tile total, then (second kernel)
+// the stripe's first position and each piece's tiles.
+__global__ __launch_bounds__(kMaxBins) void stripe_rows_kernel(const uint32_t* __restrict__ prun,
+                                                               int nb,
+                                                               uint32_t* __restrict__ rowtot) {
+  __shared__ uint64_t sh[kMaxBins / 64 + 1];
+  const int64_t s = blockIdx.x;
+  const uint32_t b = threadIdx.x;
+  const uint64_t my = b < (uint32_t)nb ? (prun[s * kMaxBins + b] + kTile - 1) / kTile : 0;
+  uint64_t tot;
+  block_excl_scan<kMaxBins>(my, sh, &tot);
+  if (b == 0) rowtot[s] = (uint32_t)tot;
+}
+
+__global__ __launch_bounds__(kMaxBins) void stripe_order_kernel(
     const uint32_t* __restrict__ prun, const uint32_t* __restrict__ ptile,
-    const uint32_t* __restrict__ btile, int64_t nstripes, int nb, int32_t* __restrict__ torder) {
-  __shared__ uint64_t sh[1024 / 64 + 1];
-  uint64_t carry = 0;
-  for (int64_t s0 = 0; s0 < nstripes; s0 += 1024) {
-    const int64_t s = s0 + threadIdx.x;
-    uint64_t row = 0;
-    if (s < nstripes)
-      for (int b = 0; b < nb; b++) row += (prun[s * kMaxBins + b] + kTile - 1) / kTile;
-    uint64_t tot;
-    uint64_t pos = carry + block_excl_scan<1024>(row, sh, &tot);
-    if (s < nstripes)
-      for (int b = 0; b < nb; b++) {
-        const uint32_t len = prun[s * kMaxBins + b];
-        const uint32_t t = btile[b] + ptile[s * kMaxBins + b];
-        for (uint32_t c = 0; c * (uint32_t)kTile < len; c++) torder[pos++] = (int32_t)(t + c);
-      }
-    carry += tot;
+    const uint32_t* __restrict__ btile, const uint32_t* __restrict__ rowtot, int nb,
+    int32_t* __restrict__ torder) {
+  __shared__ uint64_t sh[kMaxBins / 64 + 1];
+  const int64_t s = blockIdx.x;
+  const uint32_t b = threadIdx.x;
+  uint64_t before = 0;  // tiles of the stripes before s
+  for (int64_t i = b; i < s; i += kMaxBins) before += rowtot[i];
+  uint64_t base;
+  block_excl_scan<kMaxBins>(before, sh, &base);
+  const uint32_t len = b < (uint32_t)nb ? prun[s * kMaxBins + b] : 0u;
+  const uint64_t my = (len + kTile - 1) / kTile;
+  uint64_t tot;
+  uint64_t pos = base + block_excl_scan<kMaxBins>(my, sh, &tot);
+  if (my) {
+    const uint32_t t = btile[b] + ptile[s * kMaxBins + b];
+    for (uint32_t c = 0; c < (uint32_t)my; c++) torder[pos + c] = (int32_t)(t + c);
   }
 }
 
@@ -2740,14 +2752,20 @@ void launch_stripe_tables(const uint32_t* prun, int64_t nstripes, int nb, uint32
                           uint64_t* btot, uint32_t* bnt, int rbits, int buf, Seg* big,
                           int32_t* nt_over, uint32_t* btile, ListCounters* ctr,
                           const uint64_t* sbase, const SegPlan* plan, GTile* gt,
-                          const int32_t* lut_rbits, hipStream_t st, int32_t* torder) {
+                          const int32_t* lut_rbits, hipStream_t st, int32_t* torder,
+                          int64_t tiles_cap) {
   stripe_tiles_kernel<<<(unsigned)nb, kStripeThreads, 0, st>>>(prun, nstripes, ptile, btot, bnt);
   stripe_segs_kernel<<<1, kMaxBins, 0, st>>>(btot, bnt, nb, rbits, buf, big, nt_over, btile, ctr,
                                              lut_rbits);
   const int64_t np = nstripes * nb;
   stripe_gtile_kernel<<<(unsigned)((np + 255) / 256), 256, 0, st>>>(prun, ptile, btile, sbase,
                                                                     plan, nstripes, nb, gt);
-  if (torder) stripe_order_kernel<<<1, 1024, 0, st>>>(prun, ptile, btile, nstripes, nb, torder);
+  if (torder) {
+    uint32_t* rowtot = (uint32_t*)(torder + tiles_cap);
+    stripe_rows_kernel<<<(unsigned)nstripes, kMaxBins, 0, st>>>(prun, nb, rowtot);
+    stripe_order_kernel<<<(unsigned)nstripes, kMaxBins, 0, st>>>(prun, ptile, btile, rowtot, nb,
+                                                                 torder);
+  }
 }
 
 void launch_local(int key_size, const SortDesc* d, const Seg* segs, int64_t nsegs, int big_class,
