@@ -325,12 +325,14 @@ int plan_balanced_level(Workspace* W, const Request& R, const SortDesc& d, bool*
   *spread = false;
   const int ks = key_size_of(R.kind);
   const int64_t n = R.num;
-  if (R.nsegs > 0 || R.aos || n < kBalancedMinN || ks < 4) return SRS_OK;
+  if (R.nsegs > 0 || n < kBalancedMinN || ks < 4) return SRS_OK;
   const int64_t blocks = std::min<int64_t>(kSampleMaxChunks, n / kSampleChunk);
   const int64_t stride = n / blocks;
   // shist: the 64K-bin histogram, then the workgroups' partial rows
   SRS_TRY(ensure(W->shist, 65536 * sizeof(uint32_t) + sample_partial_bytes()));
-  if (!launch_sample_hist16(R.in_cols[0], ks, n, stride, kSampleChunk, blocks, d.mpos, d.mneg,
+  // (AoS records: the key at offset 0 of each record)
+  if (!launch_sample_hist16(R.in_cols[0], ks, R.aos ? (int)R.elem_size : ks, n, stride,
+                            kSampleChunk, blocks, d.mpos, d.mneg,
                             (uint32_t*)W->shist.p + 65536, (uint32_t*)W->shist.p, st))
     return fail(SRS_ERR_INTERNAL, "sample histogram: too many keys per workgroup");
   std::vector<uint32_t> h(65536);
@@ -348,6 +350,7 @@ int plan_balanced_level(Workspace* W, const Request& R, const SortDesc& d, bool*
     *spread = true;
     return SRS_OK;
   }
+  if (R.aos) return SRS_OK;  // (the digit table is not used for AoS records)
   // bins -> groups: group of bin b = floor(G * (keys before b + half of b) / total)
   std::vector<int32_t> lut(65536), first(kGroups, -1), last(kGroups, -1), rbits(kGroups);
   double before = 0;

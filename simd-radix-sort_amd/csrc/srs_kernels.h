@@ -60,9 +60,9 @@ void launch_small_sort(int key_size, const SortDesc& d, Seg g, int64_t* taken, h
 void launch_local_lsd(int key_size, const SortDesc* d, const Seg* segs,
                       const unsigned long long* nsegs, int grid, hipStream_t st);
 int64_t sample_partial_bytes();
-bool launch_sample_hist16(const void* keys, int key_bytes, int64_t n, int64_t stride, int chunk,
-                          int64_t blocks, uint64_t mpos, uint64_t mneg, uint32_t* partial,
-                          uint32_t* hist, hipStream_t st);
+bool launch_sample_hist16(const void* keys, int key_bytes, int elem_bytes, int64_t n,
+                          int64_t stride, int chunk, int64_t blocks, uint64_t mpos, uint64_t mneg,
+                          uint32_t* partial, uint32_t* hist, hipStream_t st);
 void launch_fill(int64_t n, int kind, uint64_t seed, uint64_t first, void* keys,
                  int npay, const Col* pays, hipStream_t st);
 void launch_set_desc(const SortDesc& d, SortDesc* out, hipStream_t st);

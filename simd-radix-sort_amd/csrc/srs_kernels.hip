@@ -2554,8 +2554,8 @@ __global__ __launch_bounds__(kLocalThreads) void small_sort_kernel(const SortDes
 constexpr int kSampleThreads = 1024;
 
 __global__ __launch_bounds__(kSampleThreads) void sample_hist16_kernel(
-    const char* __restrict__ keys, int key_bytes, int64_t n, int64_t stride, int chunk,
-    int64_t nchunks, uint64_t mpos, uint64_t mneg, uint32_t* __restrict__ partial) {
+    const char* __restrict__ keys, int key_bytes, int elem_bytes, int64_t n, int64_t stride,
+    int chunk, int64_t nchunks, uint64_t mpos, uint64_t mneg, uint32_t* __restrict__ partial) {
   __shared__ uint32_t h2[32768];
   for (uint32_t i = threadIdx.x; i < 32768u; i += kSampleThreads) h2[i] = 0;
   __syncthreads();
@@ -2564,7 +2564,7 @@ __global__ __launch_bounds__(kSampleThreads) void sample_hist16_kernel(
     const int64_t a = c * stride;
     const int64_t e = min(n, a + chunk);
     for (int64_t i = a + threadIdx.x; i < e; i += kSampleThreads) {
-      const uint64_t bits = load_w(keys + i * key_bytes, key_bytes);
+      const uint64_t bits = load_w(keys + i * elem_bytes, key_bytes);  // (AoS: record stride)
       const uint64_t u = bits ^ (((bits >> (kb - 1)) & 1) ? mneg : mpos);
       const uint32_t d = (uint32_t)(u >> (kb - 16)) & 0xFFFFu;
       atomicAdd(&h2[d >> 1], 1u << ((d & 1) << 4));
@@ -2590,14 +2590,14 @@ __global__ __launch_bounds__(256) void sample_reduce_kernel(const uint32_t* __re
 
 int64_t sample_partial_bytes() { return (int64_t)kSampleWGs * 32768 * 4; }
 
-bool launch_sample_hist16(const void* keys, int key_bytes, int64_t n, int64_t stride, int chunk,
-                          int64_t blocks, uint64_t mpos, uint64_t mneg, uint32_t* partial,
-                          uint32_t* hist, hipStream_t st) {
+bool launch_sample_hist16(const void* keys, int key_bytes, int elem_bytes, int64_t n,
+                          int64_t stride, int chunk, int64_t blocks, uint64_t mpos, uint64_t mneg,
+                          uint32_t* partial, uint32_t* hist, hipStream_t st) {
   const int wgs = (int)std::min<int64_t>(kSampleWGs, std::max<int64_t>(1, blocks));
   // the packed u16 bins of one workgroup must not carry into their neighbour
   if ((blocks + wgs - 1) / wgs * (int64_t)chunk >= 65536) return false;
   sample_hist16_kernel<<<(unsigned)wgs, kSampleThreads, 0, st>>>(
-      (const char*)keys, key_bytes, n, stride, chunk, blocks, mpos, mneg, partial);
+      (const char*)keys, key_bytes, elem_bytes, n, stride, chunk, blocks, mpos, mneg, partial);
   sample_reduce_kernel<<<32768 / 256, 256, 0, st>>>(partial, wgs, hist);
   return true;
 }

@@ -688,7 +688,7 @@ def test_stripe_first_level_layouts(case):
     idx = torch.arange(n, dtype=torch.int64, device="cuda")
     if case == "aos8":  # DataElement<int32, int32>: one 8-byte column
         keys = torch.randint(-2**31, 2**31 - 1, (n,), dtype=torch.int32, device="cuda",
-                             generator=g) >> 8
+                             generator=g) & ~0xFF  # duplicates, top bits spread
         rec = torch.stack([keys, idx.to(torch.int32)], dim=1).contiguous()
         out = torch.empty_like(rec)
         srs_amd.sort_combined_device(rec, srs_amd.KEY_I32, out=out)
@@ -699,7 +699,7 @@ def test_stripe_first_level_layouts(case):
         words = 4 if case == "aos32_down" else 2
         up = case != "aos32_down"
         keys = torch.randint(-2**63, 2**63 - 1, (n,), dtype=torch.int64, device="cuda", generator=g)
-        keys = keys >> 40  # duplicates: equal keys must keep input order
+        keys = keys & ~((1 << 40) - 1)  # duplicates (equal keys keep input order), top bits spread
         rec = torch.stack([keys] + [idx * (w + 1) for w in range(words - 1)], dim=1).contiguous()
         ov = keys if up else ~keys
         _, ref_i = torch.sort(ov, stable=True)
