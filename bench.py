@@ -55,10 +55,19 @@ def parse():
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--shard", action="store_true",
                     help="run the multi-GPU shard protocol even at one rank (RCCL, world 1)")
+    ap.add_argument("--extra", default="c2,c3",
+                    help="comma list of further configs measured after the headline one and "
+                         "reported under 'extra' (world 1, c1 headline only; 'none' = skip)")
+    ap.add_argument("--dry-run-launch", action="store_true",
+                    help="with --gpus N > 1 and no WORLD_SIZE: print the launcher's argv and "
+                         "env as JSON instead of starting the ranks")
     ap.add_argument("--dist", default="uniform", choices=DISTS,
                     help="key distribution (the reference's InputDistribution kinds, "
                          "src/data.hpp:64-73; c1 only; payload = f(key) as always)")
-    return ap.parse_args()
+    argv = sys.argv[1:]
+    if argv[:1] == ["--"]:  # the launcher's separator (launcher_cmd)
+        argv = argv[1:]
+    return ap.parse_args(argv)
 
 
 DISTS = ("uniform", "gaussian", "zero", "zeroone", "sorted", "reverse", "almostsorted",
@@ -136,8 +145,8 @@ def kind_id(name):
 def cpu_baseline(cfg_name, n_sample):
     sys.path.insert(0, os.path.join(REPO, "tests"))
     import numpy as np
-    from srs_testlib import (KIND_DTYPES, oracle_sort_aos, oracle_sort_soa, ref_lib,
-                             ref_sort_aos, ref_sort_soa)
+    from srs_testlib import (oracle_sort_aos, oracle_sort_soa, ref_lib, ref_sort_aos,
+                             ref_sort_soa_timed)
     kname, psizes, layout, _ = CONFIGS[cfg_name]
     kind = {"u64": 6, "f32": 8, "u32": 4}[kname]
     n = int(n_sample)
@@ -162,16 +171,24 @@ def cpu_baseline(cfg_name, n_sample):
         {4: np.uint32, 8: np.uint64}[s]) for c, s in enumerate(psizes)]
     del bits, h
     use_ref = ref_lib() is not None
-    t0 = time.perf_counter()
+    cpu_ns = None
     if layout == "aos":
         rec = np.empty((n, 16), np.uint8)
         rec[:, :8] = keys.view(np.uint8).reshape(n, 8)
         rec[:, 8:] = pays[0].view(np.uint8).reshape(n, 8)
         t0 = time.perf_counter()
+        c0 = time.process_time()
         (ref_sort_aos if use_ref else oracle_sort_aos)(kind, True, rec)
+        cpu_ns = (time.process_time() - c0) * 1e9
+    elif use_ref:
+        t0 = time.perf_counter()
+        # CLOCK_PROCESS_CPUTIME_ID around the sort call only (src/perf.hpp:33-46)
+        cpu_ns = ref_sort_soa_timed(kind, True, keys, pays)
     else:
         t0 = time.perf_counter()
-        (ref_sort_soa if use_ref else oracle_sort_soa)(kind, True, keys, pays)
+        c0 = time.process_time()
+        oracle_sort_soa(kind, True, keys, pays)
+        cpu_ns = (time.process_time() - c0) * 1e9
     dt = time.perf_counter() - t0
     try:
         model = [l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo")
@@ -183,17 +200,58 @@ def cpu_baseline(cfg_name, n_sample):
         "unit": "Gkeys/s",
         "cores": 1,
         "kind": "reference" if use_ref else "port",
-        "sample": (f"{n} keys of the same {cfg_name} workload (same generator), one sort, "
-                   f"{dt:.2f} s single-threaded on 1 core of '{model}' "
-                   f"(nproc={os.cpu_count()}); reference = jonicho radixSort.hpp "
+        "cpu_time_s": round(cpu_ns / 1e9, 3),
+        "value_cpu_time": n / (cpu_ns / 1e9) / 1e9,
+        "sample": (f"bounded sample, not the 1e9 config: {n} keys of the same {cfg_name} "
+                   f"workload (same generator), one sort, {dt:.2f} s wall / "
+                   f"{cpu_ns / 1e9:.2f} s CLOCK_PROCESS_CPUTIME_ID, single-threaded on 1 core "
+                   f"of '{model}' (nproc={os.cpu_count()}); reference = jonicho radixSort.hpp "
                    f"BitSorterSIMD AVX-512" if use_ref else
-                   f"{n} keys, C restatement (host lacks AVX-512 VBMI2), {dt:.2f} s"),
+                   f"bounded sample: {n} keys, C restatement (host lacks AVX-512 VBMI2), "
+                   f"{dt:.2f} s"),
     }
+
+
+# ---------------------------------------------------------------------------
+# --gpus N: one rank per GPU (torch.distributed.run), started before any GPU call
+# ---------------------------------------------------------------------------
+def launcher_cmd(args, argv):
+    """argv + env of the child that runs N ranks of this script. The parent
+    never imports torch or touches the GPU; it only waits for the child."""
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    fwd = [a for a in argv if a != "--dry-run-launch"]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr=127.0.0.1",
+           f"--master-port={port}", os.path.abspath(__file__), "--"] + fwd
+    # ("--": torchrun's parser would otherwise take bench options that prefix
+    # its own, e.g. --n for --nnodes, as ambiguous; parse() drops it)
+    env = dict(os.environ)
+    env["HSA_ENABLE_IPC_MODE_LEGACY"] = "0"  # dmabuf IPC only on this pool (RCCL)
+    env["MASTER_ADDR"] = "127.0.0.1"
+    return cmd, env
+
+
+def launch(args, argv):
+    cmd, env = launcher_cmd(args, argv)
+    if args.dry_run_launch:
+        print(json.dumps({"argv": cmd, "env": {k: env[k] for k in
+                                               ("HSA_ENABLE_IPC_MODE_LEGACY", "MASTER_ADDR")}}))
+        return 0
+    # rank 0 prints the JSON line on the inherited stdout
+    return subprocess.run(cmd, env=env).returncode
 
 
 # ---------------------------------------------------------------------------
 def main():
     args = parse()
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        sys.exit(launch(args, sys.argv[1:]))
+    if env_world is not None and int(env_world) != args.gpus:
+        sys.exit(f"bench.py: WORLD_SIZE={env_world} but --gpus {args.gpus}; they must agree")
     import torch
     import torch.distributed as dist
 
@@ -202,6 +260,11 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    ndev = torch.cuda.device_count()
+    if world > ndev:
+        print(f"bench.py: --gpus {world} needs {world} GPUs on this node, {ndev} visible",
+              file=sys.stderr, flush=True)
+        sys.exit(3)
     shard = world > 1 or args.shard
     if shard:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -211,7 +274,61 @@ def main():
         torch.cuda.set_device(local_rank)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
     dev = torch.device("cuda", local_rank)
-    kname, psizes, layout, cdesc = CONFIGS[args.config]
+
+    res = measure(args.config, args, torch, srs_amd, dist, dev, rank, world, shard)
+
+    cpu = None
+    if rank == 0 and args.cpu_sample > 0 and (world == 1):
+        try:
+            cpu = cpu_baseline(args.config, args.cpu_sample)
+        except Exception as e:  # report, never hide
+            cpu = {"error": repr(e)}
+
+    extra = {}
+    if world == 1 and not shard and args.config == "c1" and args.dist == "uniform":
+        for name in [e for e in args.extra.split(",") if e and e != "none"]:
+            torch.cuda.empty_cache()
+            try:
+                r = measure(name, args, torch, srs_amd, dist, dev, rank, world, shard)
+            except Exception as e:  # report, never hide
+                r = {"error": repr(e)}
+            extra[name] = r
+
+    if rank == 0:
+        out = {
+            "metric": "Gkeys/s and achieved HBM GB/s (% of roofline), 1e9 uint64 key+uint64 payload",
+            "value": res["value"],
+            "unit": "Gkeys/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": res["ms_per_step"],
+            "ms_per_step_without_event_markers": res["ms_per_step_without_event_markers"],
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": res["dtype"],
+            "data": "synthetic (device splitmix64 of the global index; payload = f(key))",
+            "config": res["config"],
+            "roofline": res["roofline"],
+            "pass_model": res["pass_model"],
+            "kernels": res["kernels"],
+            "cpu_baseline": cpu,
+            "verified": res["verified"],
+        }
+        if extra:
+            out["extra"] = extra
+        print(json.dumps(out), flush=True)
+    if shard:
+        dist.destroy_process_group()
+
+
+def measure(cfg_name, args, torch, srs_amd, dist, dev, rank, world, shard):
+    """Generates the config's resident input, runs W warmup + K timed steps
+    (barrier + synchronize on both sides, max over ranks) and returns the
+    config's numbers: Gkeys/s, roofline of the dominant kernel (HIP events
+    on the sort's stream), pass-model bytes and the full-size verification."""
+    kname, psizes, layout, cdesc = CONFIGS[cfg_name]
     kind = kind_id(kname)
     n = int(args.n)
 
@@ -220,11 +337,12 @@ def main():
     keys = torch.empty(n, dtype=key_dt, device=dev)
     pays = [torch.empty(n, dtype=tdt[s], device=dev) for s in psizes]
     srs_amd.fill_synthetic_device(keys, *pays, seed=42 << 32, first_index=rank * n, key_kind=kind)
-    if args.dist != "uniform":
-        if args.config != "c1":
+    if args.dist != "uniform" and cfg_name == args.config:
+        if cfg_name != "c1":
             raise SystemExit("--dist applies to c1 (u64 keys + u64 payload)")
         make_dist_keys(keys, pays, args.dist, torch, srs_amd, kind)
     rec = rec_out = None
+    keys_out, pays_out = None, []
     if layout == "aos":
         rec = torch.stack([keys, pays[0]], dim=1).contiguous()
         rec_out = torch.empty_like(rec)
@@ -253,35 +371,42 @@ def main():
         else:
             srs_amd.sort_device(keys, *pays, key_kind=kind, out=(keys_out, *pays_out))
 
+    def sync():
+        torch.cuda.synchronize()
+        if shard:
+            dist.barrier()
+        torch.cuda.synchronize()
+
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
     srs_amd.reset_kernel_stats()
     srs_amd.set_kernel_timing(True)
-    if shard:
-        dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
-    torch.cuda.synchronize()
-    if shard:
-        dist.barrier()
+    sync()
     t1 = time.perf_counter()
     srs_amd.set_kernel_timing(False)
     elapsed = t1 - t0
     # The timed steps carry HIP event markers around each launch (async
     # stream packets, no host waits; the roofline's launch durations come
     # from them). The same steps without the markers, for comparison:
-    torch.cuda.synchronize()
-    if shard:
-        dist.barrier()
+    kstats = {}
+    for name in ("count", "scatter", "local", "local_fast", "local_stable", "local_lsd", "scan",
+                 "plan", "children", "copy", "partition", "key_hist"):
+        try:
+            l, ms, el = srs_amd.kernel_stats(name)
+        except Exception:
+            continue
+        if l:
+            kstats[name] = {"launches": l, "ms": ms, "elems": el}
+    sync()
     t2 = time.perf_counter()
     for _ in range(min(args.steps, 3)):
         step()
-    torch.cuda.synchronize()
-    if shard:
-        dist.barrier()
+    sync()
     ms_no_events = (time.perf_counter() - t2) / min(args.steps, 3) * 1e3
     if shard:
         tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
@@ -292,14 +417,9 @@ def main():
     gkeys = total_keys / elapsed / 1e9
 
     # ---- per-kernel device time (HIP events on the launch stream) ----------
-    kstats = {}
-    for name in ("count", "scatter", "local", "local_fast", "local_stable", "local_lsd", "scan",
-                 "plan", "children", "copy"):
-        l, ms, el = srs_amd.kernel_stats(name)
-        if l:
-            kstats[name] = {"launches": l, "ms": ms, "elems": el}
     ks = 8 if kname == "u64" else 4
-    per_elem = {"count": ks, "scatter": 2 * rec_bytes, "local": 2 * rec_bytes}
+    c_b = ks if layout == "soa" else rec_bytes
+    per_elem = {"count": c_b, "scatter": 2 * rec_bytes, "local": 2 * rec_bytes}
     dom = max((k for k in kstats if k in per_elem), key=lambda k: kstats[k]["ms"], default=None)
     roofline = None
     if dom:
@@ -312,59 +432,53 @@ def main():
                     "traffic": pmc_traffic(dom, cdesc, n) if world == 1 else None,
                     "bytes_per_launch": bytes_per_launch, "avg_launch_ms": round(avg_ms, 4)}
 
-    # pass-model yardstick: B_alg = n*[L_g*(c+2s)+2s]
+    # pass-model yardstick: B_alg = n*[L_g*(c+2s)+2s], and
+    # the same model with the global levels this sort actually ran (count
+    # launches per step) next to it
     import math
     s_b = rec_bytes
-    c_b = ks if layout == "soa" else rec_bytes
     L_g = min(math.ceil(math.log(max(n / 4096, 1.0001), 256)), ks)
     b_alg = n * (L_g * (c_b + 2 * s_b) + 2 * s_b)
     pass_model_gbs = b_alg * world / (elapsed / args.steps) / 1e9
+    levels_run = (kstats.get("count", {}).get("launches", 0) / args.steps) if not shard else None
+    pass_model = {"B_alg_bytes_per_gpu": b_alg, "L_g": L_g, "gbs": round(pass_model_gbs, 1),
+                  "frac_of_8TBs": round(pass_model_gbs / world / HBM_PEAK_GBS, 4)}
+    if levels_run:
+        b_run = n * (levels_run * (c_b + 2 * s_b) + 2 * s_b)
+        pass_model["global_levels_run"] = levels_run
+        pass_model["bytes_of_levels_run"] = b_run
+        pass_model["frac_of_8TBs_levels_run"] = round(
+            b_run / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBS, 4)
 
     verified = None
     if not args.no_verify and not shard:
-        verified = verify(keys_out if layout == "soa" else None, pays_out if layout == "soa" else None,
-                          rec_out, kname, psizes, torch)
+        if layout == "aos":
+            verified = verify(None, None, rec_out, kname, psizes, torch,
+                              ins=(rec[:, 0], [rec[:, 1]]))
+        else:
+            verified = verify(keys_out, pays_out, None, kname, psizes, torch, ins=(keys, pays))
     elif not args.no_verify:
         verified = verify_shards(keys, pays, shard_out[0], kname, psizes, torch, dist, dev)
+    del keys, pays, keys_out, pays_out, rec, rec_out, shard_out
 
-    cpu = None
-    if rank == 0 and args.cpu_sample > 0 and (world == 1):
-        try:
-            cpu = cpu_baseline(args.config, args.cpu_sample)
-        except Exception as e:  # report, never hide
-            cpu = {"error": repr(e)}
-
-    if rank == 0:
-        out = {
-            "metric": "Gkeys/s and achieved HBM GB/s (% of roofline), 1e9 uint64 key+uint64 payload",
-            "value": round(gkeys, 4),
-            "unit": "Gkeys/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(ms_per_step, 3),
-            "ms_per_step_without_event_markers": round(ms_no_events, 3),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": kname if kname != "u64" else "uint64",
-            "data": "synthetic (device splitmix64 of the global index; payload = f(key))",
-            "config": {"workload": args.config + ": " + cdesc +
-                       ("" if args.dist == "uniform" else f", {args.dist} keys"), "keys_per_gpu": n,
-                       "total_keys": n * world, "record_bytes": rec_bytes,
-                       "parallelism": f"top-radix-bits shard x{world}" if world > 1 else "1 GPU"},
-            "roofline": roofline,
-            "pass_model": {"B_alg_bytes_per_gpu": b_alg, "gbs": round(pass_model_gbs, 1),
-                           "frac_of_8TBs": round(pass_model_gbs / world / HBM_PEAK_GBS, 4)},
-            "kernels": {k: {"launches": v["launches"], "avg_ms": round(v["ms"] / v["launches"], 4),
-                            "total_ms_per_step": round(v["ms"] / args.steps, 3)}
-                        for k, v in kstats.items()},
-            "cpu_baseline": cpu,
-            "verified": verified,
-        }
-        print(json.dumps(out), flush=True)
-    if shard:
-        dist.destroy_process_group()
+    return {
+        "value": round(gkeys, 4),
+        "unit": "Gkeys/s",
+        "ms_per_step": round(ms_per_step, 3),
+        "ms_per_step_without_event_markers": round(ms_no_events, 3),
+        "dtype": kname if kname != "u64" else "uint64",
+        "config": {"workload": cfg_name + ": " + cdesc +
+                   ("" if args.dist == "uniform" or cfg_name != args.config
+                    else f", {args.dist} keys"), "keys_per_gpu": n,
+                   "total_keys": n * world, "record_bytes": rec_bytes,
+                   "parallelism": f"top-radix-bits shard x{world}" if world > 1 else "1 GPU"},
+        "roofline": roofline,
+        "pass_model": pass_model,
+        "kernels": {k: {"launches": v["launches"], "avg_ms": round(v["ms"] / v["launches"], 4),
+                        "total_ms_per_step": round(v["ms"] / args.steps, 3)}
+                    for k, v in kstats.items()},
+        "verified": verified,
+    }
 
 
 def _order_view(k, kname, torch):
@@ -450,11 +564,13 @@ def verify_shards(keys_in, pays_in, out, kname, psizes, torch, dist, dev):
             "count_equal": h[2].item() == h[3].item()}
 
 
-def verify(keys_out, pays_out, rec_out, kname, psizes, torch):
+def verify(keys_out, pays_out, rec_out, kname, psizes, torch, ins=None):
     """Size-independent checks on the full output: sortedness (transformed
-    order) and payload == f(key) for every element. With payload = f(key)
-    the sorted output is unique, so this is bit-exact parity at full size
-    (together with the element count, fixed by construction)."""
+    order), payload == f(key) for every element, and an order-independent
+    hash of all (key, payload) records equal to the input's (catches a
+    dropped record replaced by a duplicate of its neighbour). With payload =
+    f(key) the sorted output is unique, so this is bit-exact parity at full
+    size."""
     if rec_out is not None:
         k = rec_out[:, 0]
         p = [rec_out[:, 1]]
@@ -462,7 +578,11 @@ def verify(keys_out, pays_out, rec_out, kname, psizes, torch):
         k, p = keys_out, pays_out
     s = _order_view(k, kname, torch)
     ok = bool((s[1:] >= s[:-1]).all().item())
-    return {"sorted": ok, "payload_eq_f_key": _check_payloads(k, p, psizes, torch)}
+    res = {"sorted": ok, "payload_eq_f_key": _check_payloads(k, p, psizes, torch)}
+    if ins is not None:
+        res["multiset_hash_equal"] = _hash_pairs(ins[0], ins[1], torch) == _hash_pairs(k, p, torch)
+        res["count_equal"] = ins[0].numel() == k.numel()
+    return res
 
 
 if __name__ == "__main__":

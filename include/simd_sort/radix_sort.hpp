@@ -8,6 +8,11 @@
 //   simd_sort::radix_sort::sort<false>(num, keyArray, payloadArrays...);
 //   simd_sort::radix_sort::sort(num, (simd_sort::DataElement<K, Ps...>*) combined);
 //   simd_sort::radix_sort::sort<Up, BitSorter, CmpSorter>(cmpSortThreshold, num, ...);
+//   simd_sort::radix_sort::sort(cmpSortThreshold, num, ...);   // defaulted, :1761-1763
+//
+// BitSorter may be spelled as in radixSort.hpp (`BitSorterSIMD`, a plain
+// name) or as in src/radix_sort.hpp:109 (`BitSorterSIMD<>`,
+// `BitSorterSIMD<false>`, `BitSorterSIMD<true>` = OneReg).
 //
 // The arrays are sorted in place. Instead of the AVX-512 partition the work
 // runs as HIP kernels on the GPU through the C ABI in srs_c_api.h
@@ -27,6 +32,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 #include <tuple>
 #include <type_traits>
 
@@ -62,11 +68,12 @@ struct DataElement<K> {
 // (radixSort.hpp:159-178) becomes the GPU's LDS-resident leaf; the name is
 // kept so that existing call sites compile unchanged.
 struct CmpSorterInsertionSort {};
-// src/cmp_sorters.hpp:66-78: the reference leaves every leaf (<= threshold
-// elements) in partition order, so each element ends within
-// cmpSortThreshold of its sorted position. A leaf holds exactly the elements
-// a full sort puts there; the GPU sorts the leaves anyway (its LDS pass
-// sorts whole segments at once), which meets the same guarantee.
+// src/cmp_sorters.hpp:66-78: the recursion stops at leaves of <=
+// cmpSortThreshold elements and leaves them in partition order, so each
+// element ends within cmpSortThreshold of its sorted position (thesis
+// 3113-3124). On the GPU the local pass skips its in-bucket rank when every
+// bucket holds <= cmpSortThreshold keys (SRS_LEAF_UNSORTED); every leaf holds
+// exactly the elements a full sort puts there.
 struct CmpSorterNoSort {};
 // src/cmp_sorters.hpp:40-63 (needs the vendored bramas sorters there): the
 // leaves are sorted (as here); the reference's type restrictions are kept
@@ -75,11 +82,21 @@ struct CmpSorterBramasSmallSort {};
 
 namespace radix_sort {
 
-// Bit-sorter selectors (radixSort.hpp:1583 BitSorterSIMD; src/radix_sort.hpp:66
-// BitSorterSequential). Both produce the same key order; on the GPU both run
+// Bit-sorter selectors. src/radix_sort.hpp:109 declares
+// `template <bool OneReg = false> struct BitSorterSIMD` (OneReg: one
+// register per payload vector, :119-121); radixSort.hpp:1583 has the plain
+// `struct BitSorterSIMD`. Here it is the class template, and the sort()
+// overloads below also take the template itself as a template-template
+// argument, so both spellings compile. BitSorterSequential is
+// src/radix_sort.hpp:66. All produce the same key order; on the GPU all run
 // the same multi-bit digit passes.
-struct BitSorterSIMD {};
-struct BitSorterSequential {};
+template <bool OneReg = false>
+struct BitSorterSIMD {
+  static std::string name() { return OneReg ? "BitSorterSIMD<OneReg>" : "BitSorterSIMD"; }
+};
+struct BitSorterSequential {
+  static std::string name() { return "BitSorterSequential"; }
+};
 
 namespace detail {
 
@@ -109,8 +126,13 @@ inline constexpr bool known_cmp_sorter = std::is_same_v<CmpSorter, CmpSorterInse
                                          std::is_same_v<CmpSorter, CmpSorterNoSort> ||
                                          std::is_same_v<CmpSorter, CmpSorterBramasSmallSort>;
 
+template <typename CmpSorter>
+inline constexpr int leaf_mode =
+    std::is_same_v<CmpSorter, CmpSorterNoSort> ? SRS_LEAF_UNSORTED : SRS_LEAF_SORTED;
+
 template <typename BitSorter>
-inline constexpr bool known_bit_sorter = std::is_same_v<BitSorter, BitSorterSIMD> ||
+inline constexpr bool known_bit_sorter = std::is_same_v<BitSorter, BitSorterSIMD<false>> ||
+                                         std::is_same_v<BitSorter, BitSorterSIMD<true>> ||
                                          std::is_same_v<BitSorter, BitSorterSequential>;
 
 // src/cmp_sorters.hpp:47-61
@@ -144,7 +166,9 @@ inline void check(int rc, const char* what) {
 }  // namespace detail
 
 // sort(cmpSortThreshold, num, keys, payloads...) — radixSort.hpp:1761-1768
-template <bool Up, typename BitSorter, typename CmpSorter, typename K, typename... Ps>
+// (defaults as there: Up = true, BitSorterSIMD, CmpSorterInsertionSort)
+template <bool Up = true, typename BitSorter = BitSorterSIMD<>,
+          typename CmpSorter = CmpSorterInsertionSort, typename K, typename... Ps>
 void sort(SortIndex cmpSortThreshold, const SortIndex num, K* const keys,
           Ps* const... payloads) {
   static_assert(detail::known_bit_sorter<BitSorter>,
@@ -157,14 +181,17 @@ void sort(SortIndex cmpSortThreshold, const SortIndex num, K* const keys,
   static_assert(sizeof...(Ps) <= SRS_MAX_PAYLOADS, "too many payload arrays");
   void* pays[sizeof...(Ps) + 1] = {(void*)payloads..., nullptr};
   uint32_t sizes[sizeof...(Ps) + 1] = {(uint32_t)sizeof(Ps)..., 0};
-  detail::check(srs_sort_soa((int64_t)num, detail::key_kind<K>(), Up ? 1 : 0,
-                             (int64_t)cmpSortThreshold, (void*)keys, (int32_t)sizeof...(Ps),
-                             pays, sizes),
+  detail::check(srs_sort_soa_leaf((int64_t)num, detail::key_kind<K>(), Up ? 1 : 0,
+                                  (int64_t)cmpSortThreshold, detail::leaf_mode<CmpSorter>,
+                                  (void*)keys, (int32_t)sizeof...(Ps), pays, sizes),
                 "sort");
 }
 
 // sort(cmpSortThreshold, num, DataElement<K, Ps...>*) — radixSort.hpp:1770-1778
-template <bool Up, typename BitSorter, typename CmpSorter, typename K, typename... Ps>
+// (the reference also reaches it through the defaulted SoA form with
+// K = DataElement; partial ordering picks this overload for both)
+template <bool Up = true, typename BitSorter = BitSorterSIMD<>,
+          typename CmpSorter = CmpSorterInsertionSort, typename K, typename... Ps>
 void sort(SortIndex cmpSortThreshold, const SortIndex num,
           DataElement<K, Ps...>* const elements) {
   static_assert(detail::known_bit_sorter<BitSorter>,
@@ -177,16 +204,32 @@ void sort(SortIndex cmpSortThreshold, const SortIndex num,
   static_assert(sizeof(DataElement<K, Ps...>) <= 64, "DataElement larger than 64 bytes");
   static_assert(detail::key_kind<K>() >= 0,
                 "key type must be one of u8/i8/u16/i16/u32/i32/u64/i64/float/double");
-  detail::check(srs_sort_aos((int64_t)num, detail::key_kind<K>(), Up ? 1 : 0,
-                             (int64_t)cmpSortThreshold, (void*)elements,
-                             (uint32_t)sizeof(DataElement<K, Ps...>)),
+  detail::check(srs_sort_aos_leaf((int64_t)num, detail::key_kind<K>(), Up ? 1 : 0,
+                                  (int64_t)cmpSortThreshold, detail::leaf_mode<CmpSorter>,
+                                  (void*)elements, (uint32_t)sizeof(DataElement<K, Ps...>)),
                 "sort");
+}
+
+// The radixSort.hpp spelling sort<Up, BitSorterSIMD, CmpSorter>(...): the
+// bit sorter named without template arguments (radixSort.hpp:1583, 1764).
+template <bool Up, template <bool> class BitSorter, typename CmpSorter = CmpSorterInsertionSort,
+          typename K, typename... Ps>
+void sort(SortIndex cmpSortThreshold, const SortIndex num, K* const keys,
+          Ps* const... payloads) {
+  sort<Up, BitSorter<false>, CmpSorter>(cmpSortThreshold, num, keys, payloads...);
+}
+
+template <bool Up, template <bool> class BitSorter, typename CmpSorter = CmpSorterInsertionSort,
+          typename K, typename... Ps>
+void sort(SortIndex cmpSortThreshold, const SortIndex num,
+          DataElement<K, Ps...>* const elements) {
+  sort<Up, BitSorter<false>, CmpSorter>(cmpSortThreshold, num, elements);
 }
 
 // sort<Up>(num, keys, payloads...) — radixSort.hpp:1780-1783 (threshold 16)
 template <bool Up = true, typename K, typename... Ps>
 void sort(const SortIndex num, K* const keys, Ps* const... payloads) {
-  sort<Up, BitSorterSIMD, CmpSorterInsertionSort>(16, num, keys, payloads...);
+  sort<Up, BitSorterSIMD<>, CmpSorterInsertionSort>(16, num, keys, payloads...);
 }
 
 // ---- device-resident extension (no reference counterpart) ----------------

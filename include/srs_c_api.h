@@ -94,6 +94,27 @@ int srs_sort_soa(int64_t num, int key_kind, int up, int64_t cmp_sort_threshold,
 int srs_sort_aos(int64_t num, int key_kind, int up, int64_t cmp_sort_threshold,
                  void* elements, uint32_t elem_size);
 
+/* Leaf handling: the reference's CmpSorter template argument
+ * (src/cmp_sorters.hpp). SRS_LEAF_SORTED = CmpSorterInsertionSort (and
+ * CmpSorterBramasSmallSort): leaves of <= cmp_sort_threshold keys are sorted,
+ * so the output is fully sorted. SRS_LEAF_UNSORTED = CmpSorterNoSort
+ * (src/cmp_sorters.hpp:66-78, thesis:3113-3124): the recursion stops at
+ * leaves of <= cmp_sort_threshold keys and leaves them in partition order.
+ * Every leaf then holds exactly the keys (and their payloads) a full sort
+ * puts there, so each element ends within cmp_sort_threshold - 1 places of
+ * its sorted slot; num <= cmp_sort_threshold leaves the input untouched. */
+#define SRS_LEAF_SORTED 0
+#define SRS_LEAF_UNSORTED 1
+
+/* srs_sort_soa / srs_sort_aos with the leaf handling chosen by leaf_mode:
+ * sort<Up, BitSorter, CmpSorter>(cmpSortThreshold, num, ...) for every
+ * CmpSorter of src/cmp_sorters.hpp (radixSort.hpp:1761-1778). */
+int srs_sort_soa_leaf(int64_t num, int key_kind, int up, int64_t cmp_sort_threshold,
+                      int leaf_mode, void* keys, int32_t num_payloads, void* const* payloads,
+                      const uint32_t* payload_sizes);
+int srs_sort_aos_leaf(int64_t num, int key_kind, int up, int64_t cmp_sort_threshold,
+                      int leaf_mode, void* elements, uint32_t elem_size);
+
 /* ---- device-pointer entry points (asynchronous on `stream`) ------------- */
 
 /* Same as srs_sort_soa on device pointers. `stream` is a hipStream_t (NULL =
@@ -111,6 +132,15 @@ int srs_sort_soa_device(int64_t num, int key_kind, int up,
 int srs_sort_aos_device(int64_t num, int key_kind, int up,
                         int64_t cmp_sort_threshold, void* elements,
                         uint32_t elem_size, void* elements_out, void* stream);
+
+/* The device forms with the leaf handling chosen by leaf_mode (see above). */
+int srs_sort_soa_device_leaf(int64_t num, int key_kind, int up, int64_t cmp_sort_threshold,
+                             int leaf_mode, void* keys, int32_t num_payloads,
+                             void* const* payloads, const uint32_t* payload_sizes,
+                             void* keys_out, void* const* payloads_out, void* stream);
+int srs_sort_aos_device_leaf(int64_t num, int key_kind, int up, int64_t cmp_sort_threshold,
+                             int leaf_mode, void* elements, uint32_t elem_size,
+                             void* elements_out, void* stream);
 
 /* Sorts each segment [segment_bounds[i], segment_bounds[i+1]) of a device
  * key column and its payload columns independently, in place, as sub-ranges

@@ -273,7 +273,15 @@ struct Request {
   const int64_t* seg_bounds = nullptr;  // optional: sort [b[i], b[i+1]) independently
   int64_t nsegs = 0;
   int known_top_bits = 0;               // every segment's keys agree on these top bits
+  int leaf_mode = SRS_LEAF_SORTED;      // SRS_LEAF_UNSORTED: CmpSorterNoSort
 };
+
+// SortDesc::leaf_skip of a request: CmpSorterNoSort leaves every leaf of
+// <= cmpSortThreshold keys in partition order (src/cmp_sorters.hpp:66-78)
+int32_t leaf_skip_of(const Request& R) {
+  if (R.leaf_mode != SRS_LEAF_UNSORTED || R.thresh <= 1) return 0;
+  return (int32_t)std::min<int64_t>(R.thresh, 65535);
+}
 
 void key_masks(int kind, int up, SortDesc& d) {
   const int kb = 8 * key_size_of(kind);
@@ -623,6 +631,7 @@ int run_small(Workspace* W, const Request& R, hipStream_t st) {
   key_masks(R.kind, R.up, d);
   const bool is_float = R.kind == SRS_KEY_F32 || R.kind == SRS_KEY_F64;
   d.canon_zero = (is_float && n <= R.thresh) ? 1 : 0;
+  d.leaf_skip = leaf_skip_of(R);
   const int ksl = ks | (d.canon_zero ? SRS_KS_CANON : 0);
   set_columns(R, d, nullptr, nullptr, false, 0, nullptr, inplace);
   d.stamp_acc = g_stamp_acc;
@@ -661,6 +670,7 @@ int run_sort(Workspace* W, const Request& R, hipStream_t st) {
   key_masks(R.kind, R.up, d);
   const bool is_float = R.kind == SRS_KEY_F32 || R.kind == SRS_KEY_F64;
   d.canon_zero = (is_float && n <= R.thresh) ? 1 : 0;
+  d.leaf_skip = leaf_skip_of(R);
   const int ksl = ks | (d.canon_zero ? SRS_KS_CANON : 0);  // kernel dispatch key
 
   // AoS records of 16+ bytes travel as SoA slice columns through the
@@ -989,8 +999,14 @@ int copy_through(const Request& R, hipStream_t st) {
   return SRS_OK;
 }
 
+// CmpSorterNoSort with num <= cmpSortThreshold: the whole input is one leaf,
+// which the reference leaves as it is (radixSort.hpp:1743, cmp_sorters.hpp:66-78)
+bool whole_input_is_unsorted_leaf(const Request& R) {
+  return R.leaf_mode == SRS_LEAF_UNSORTED && R.num <= R.thresh;
+}
+
 int sort_device(Request& R, hipStream_t st) {
-  if (R.num <= 1) return copy_through(R, st);
+  if (R.num <= 1 || whole_input_is_unsorted_leaf(R)) return copy_through(R, st);
   std::lock_guard<std::mutex> lk(g_wmu);
   Workspace* W = nullptr;
   SRS_TRY(get_ws(&W));
@@ -1001,7 +1017,7 @@ int sort_device(Request& R, hipStream_t st) {
 }
 
 int sort_host(Request& R) {
-  if (R.num <= 1) return SRS_OK;
+  if (R.num <= 1 || whole_input_is_unsorted_leaf(R)) return SRS_OK;
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
     return fail(SRS_ERR_NO_DEVICE, "no HIP device available");
@@ -1106,6 +1122,13 @@ int build_aos(Request& R, int64_t num, int kind, int up, int64_t thresh, void* e
   return SRS_OK;
 }
 
+int set_leaf_mode(Request& R, int leaf_mode) {
+  if (leaf_mode != SRS_LEAF_SORTED && leaf_mode != SRS_LEAF_UNSORTED)
+    return fail(SRS_ERR_INVALID_ARG, "leaf_mode must be SRS_LEAF_SORTED or SRS_LEAF_UNSORTED");
+  R.leaf_mode = leaf_mode;
+  return SRS_OK;
+}
+
 }  // namespace
 }  // namespace srs
 
@@ -1126,6 +1149,47 @@ int srs_sort_aos(int64_t num, int key_kind, int up, int64_t cmp_sort_threshold,
   Request R;
   SRS_TRY(build_aos(R, num, key_kind, up, cmp_sort_threshold, elements, elem_size, nullptr));
   return sort_host(R);
+}
+
+int srs_sort_soa_leaf(int64_t num, int key_kind, int up, int64_t cmp_sort_threshold,
+                      int leaf_mode, void* keys, int32_t num_payloads, void* const* payloads,
+                      const uint32_t* payload_sizes) {
+  Request R;
+  SRS_TRY(build_soa(R, num, key_kind, up, cmp_sort_threshold, keys, num_payloads, payloads,
+                    payload_sizes, nullptr, nullptr));
+  SRS_TRY(set_leaf_mode(R, leaf_mode));
+  return sort_host(R);
+}
+
+int srs_sort_aos_leaf(int64_t num, int key_kind, int up, int64_t cmp_sort_threshold,
+                      int leaf_mode, void* elements, uint32_t elem_size) {
+  Request R;
+  SRS_TRY(build_aos(R, num, key_kind, up, cmp_sort_threshold, elements, elem_size, nullptr));
+  SRS_TRY(set_leaf_mode(R, leaf_mode));
+  return sort_host(R);
+}
+
+int srs_sort_soa_device_leaf(int64_t num, int key_kind, int up, int64_t cmp_sort_threshold,
+                             int leaf_mode, void* keys, int32_t num_payloads,
+                             void* const* payloads, const uint32_t* payload_sizes,
+                             void* keys_out, void* const* payloads_out, void* stream) {
+  Request R;
+  SRS_TRY(build_soa(R, num, key_kind, up, cmp_sort_threshold, keys, num_payloads, payloads,
+                    payload_sizes, keys_out, payloads_out));
+  SRS_TRY(set_leaf_mode(R, leaf_mode));
+  SRS_TRY(check_device_alignment(R));
+  return sort_device(R, (hipStream_t)stream);
+}
+
+int srs_sort_aos_device_leaf(int64_t num, int key_kind, int up, int64_t cmp_sort_threshold,
+                             int leaf_mode, void* elements, uint32_t elem_size,
+                             void* elements_out, void* stream) {
+  Request R;
+  SRS_TRY(build_aos(R, num, key_kind, up, cmp_sort_threshold, elements, elem_size,
+                    elements_out));
+  SRS_TRY(set_leaf_mode(R, leaf_mode));
+  SRS_TRY(check_device_alignment(R));
+  return sort_device(R, (hipStream_t)stream);
 }
 
 int srs_sort_soa_device(int64_t num, int key_kind, int up, int64_t cmp_sort_threshold,

@@ -53,6 +53,9 @@ struct SortDesc {
                            // are one interleaved 8-byte word per record in
                            // TMP / TMP2 (stride 8, col 2 at +4; tmp2 is set),
                            // separate arrays in IN / OUT
+  int32_t leaf_skip;       // CmpSorterNoSort (src/cmp_sorters.hpp:66-78): the local
+                           // pass leaves buckets of <= leaf_skip keys in bucket-pass
+                           // order instead of ranking them (0: leaves sorted)
   // transformed key u = bits ^ (bits & signbit ? mneg : mpos)
   uint64_t mpos, mneg, signbit, negzero;
   // partition passes only: digit = digit_lut[u >> lut_shift]

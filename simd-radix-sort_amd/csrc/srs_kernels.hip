@@ -1819,7 +1819,11 @@ __device__ __forceinline__ bool local_fast_body(const SortDesc* __restrict__ des
     }
     lds_barrier();
     STAMP();  // 2: bucket histogram
-    if (maxlen > kRankSortMax) {
+    // CmpSorterNoSort: when every bucket (a node of the reference's bit
+    // recursion, all keys sharing the bits above sh) holds <= leaf_skip keys,
+    // the buckets are the leaves and stay in bucket-pass order
+    const bool skip_rank = maxlen <= desc->leaf_skip;
+    if (maxlen > kRankSortMax && !skip_rank) {
       // a large bucket (duplicates or skew): local_stable_kernel takes the
       // segment (nothing has been written to global memory yet)
       bail();
@@ -1839,6 +1843,12 @@ __device__ __forceinline__ bool local_fast_body(const SortDesc* __restrict__ des
     if (threadIdx.x < (uint32_t)kRankSortMax) sbuf[cnt + threadIdx.x] = ~0ull;  // sentinels
     lds_barrier();
     STAMP();  // 3: bucket scatter
+    if (skip_rank) {  // the leaves unsorted: output slot p takes word p
+      for (int p = (int)threadIdx.x; p < cnt; p += NT)
+        perm[p] = DIRECT ? (uint16_t)p : (uint16_t)(sbuf[p] & ((1u << IDXB) - 1));
+      lds_barrier();
+      return false;
+    }
     // ---- 3. rank inside each bucket: #(words of the bucket below mine) ----
     // The word orders by (key, original index), so the result is stable.
     // Slots in two halves bound register use; a wave-uniform trip count

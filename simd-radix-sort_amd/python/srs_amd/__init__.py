@@ -38,6 +38,9 @@ _NP_KIND = {np.dtype(np.uint8): KEY_U8, np.dtype(np.int8): KEY_I8,
             np.dtype(np.float32): KEY_F32, np.dtype(np.float64): KEY_F64}
 
 SRS_OK = 0
+# leaf handling (srs_c_api.h): the reference's CmpSorter (src/cmp_sorters.hpp)
+LEAF_SORTED, LEAF_UNSORTED = 0, 1
+_LEAF = {"insertion": LEAF_SORTED, "bramas": LEAF_SORTED, "nosort": LEAF_UNSORTED}
 
 
 class SrsError(RuntimeError):
@@ -58,6 +61,13 @@ def lib() -> ctypes.CDLL:
     i64, i32, u32, vp = ctypes.c_int64, ctypes.c_int32, ctypes.c_uint32, ctypes.c_void_p
     L.srs_sort_soa.argtypes = [i64, ctypes.c_int, ctypes.c_int, i64, vp, i32, vp, vp]
     L.srs_sort_aos.argtypes = [i64, ctypes.c_int, ctypes.c_int, i64, vp, u32]
+    L.srs_sort_soa_leaf.argtypes = [i64, ctypes.c_int, ctypes.c_int, i64, ctypes.c_int, vp, i32,
+                                    vp, vp]
+    L.srs_sort_aos_leaf.argtypes = [i64, ctypes.c_int, ctypes.c_int, i64, ctypes.c_int, vp, u32]
+    L.srs_sort_soa_device_leaf.argtypes = [i64, ctypes.c_int, ctypes.c_int, i64, ctypes.c_int, vp,
+                                           i32, vp, vp, vp, vp, vp]
+    L.srs_sort_aos_device_leaf.argtypes = [i64, ctypes.c_int, ctypes.c_int, i64, ctypes.c_int, vp,
+                                           u32, vp, vp]
     L.srs_sort_soa_device.argtypes = [i64, ctypes.c_int, ctypes.c_int, i64, vp, i32, vp, vp,
                                       vp, vp, vp]
     L.srs_sort_aos_device.argtypes = [i64, ctypes.c_int, ctypes.c_int, i64, vp, u32, vp, vp]
@@ -107,20 +117,28 @@ def _size_array(sizes):
 # --------------------------------------------------------------------------
 # host arrays (drop-in semantics: in place, synchronous)
 # --------------------------------------------------------------------------
+def _leaf(cmp_sorter: str) -> int:
+    if cmp_sorter not in _LEAF:
+        raise ValueError(f"cmp_sorter must be one of {sorted(_LEAF)}")
+    return _LEAF[cmp_sorter]
+
+
 def sort_thresh(cmp_sort_threshold: int, keys: np.ndarray, *payloads: np.ndarray,
-                up: bool = True) -> None:
-    """radix_sort::sort<Up, BitSorterSIMD, CmpSorterInsertionSort>(thresh, num,
-    keys, payloads...) on host numpy arrays, in place."""
+                up: bool = True, cmp_sorter: str = "insertion") -> None:
+    """radix_sort::sort<Up, BitSorterSIMD, CmpSorter>(thresh, num, keys,
+    payloads...) on host numpy arrays, in place. cmp_sorter: "insertion"
+    (CmpSorterInsertionSort), "bramas" (sorted leaves as well) or "nosort"
+    (CmpSorterNoSort: leaves of <= thresh keys stay in partition order)."""
     n = len(keys)
     for a in (keys,) + payloads:
         if not (isinstance(a, np.ndarray) and a.flags.c_contiguous and a.ndim == 1):
             raise ValueError("arrays must be 1-D C-contiguous numpy arrays")
         if len(a) != n:
             raise ValueError("all arrays must have the same length")
-    _check(lib().srs_sort_soa(n, key_kind_of(keys.dtype), int(bool(up)), int(cmp_sort_threshold),
-                              keys.ctypes.data, len(payloads),
-                              _ptr_array([p.ctypes.data for p in payloads]),
-                              _size_array([p.dtype.itemsize for p in payloads])))
+    _check(lib().srs_sort_soa_leaf(n, key_kind_of(keys.dtype), int(bool(up)),
+                                   int(cmp_sort_threshold), _leaf(cmp_sorter), keys.ctypes.data,
+                                   len(payloads), _ptr_array([p.ctypes.data for p in payloads]),
+                                   _size_array([p.dtype.itemsize for p in payloads])))
 
 
 def sort(keys: np.ndarray, *payloads: np.ndarray, up: bool = True) -> None:
@@ -129,7 +147,7 @@ def sort(keys: np.ndarray, *payloads: np.ndarray, up: bool = True) -> None:
 
 
 def sort_combined(elements: np.ndarray, key_kind: int, up: bool = True,
-                  cmp_sort_threshold: int = 16) -> None:
+                  cmp_sort_threshold: int = 16, cmp_sorter: str = "insertion") -> None:
     """radix_sort::sort(num, (DataElement<K, Ps...>*) combined): `elements` is a
     C-contiguous array whose rows are records (2-D uint8 (n, elem_size), or a
     structured / plain 1-D array); the key of kind `key_kind` is at byte 0."""
@@ -137,8 +155,8 @@ def sort_combined(elements: np.ndarray, key_kind: int, up: bool = True,
         raise ValueError("elements must be C-contiguous")
     n = elements.shape[0]
     esz = elements.nbytes // n if n else elements.dtype.itemsize
-    _check(lib().srs_sort_aos(n, int(key_kind), int(bool(up)), int(cmp_sort_threshold),
-                              elements.ctypes.data, esz))
+    _check(lib().srs_sort_aos_leaf(n, int(key_kind), int(bool(up)), int(cmp_sort_threshold),
+                                   _leaf(cmp_sorter), elements.ctypes.data, esz))
 
 
 # --------------------------------------------------------------------------
@@ -185,7 +203,8 @@ def _check_columns(keys, cols, what="tensors"):
 
 
 def sort_device(keys, *payloads, up: bool = True, cmp_sort_threshold: int = 16,
-                key_kind: int | None = None, out=None, stream=None) -> None:
+                key_kind: int | None = None, out=None, stream=None,
+                cmp_sorter: str = "insertion") -> None:
     """Sort device tensors. In place unless `out` = (keys_out, *payloads_out).
     `key_kind` overrides the kind derived from keys.dtype (e.g. torch.int64
     storage holding uint64 keys). Runs on keys' GPU, on `stream` or that
@@ -207,9 +226,10 @@ def sort_device(keys, *payloads, up: bool = True, cmp_sort_threshold: int = 16,
     else:
         kout, pout = None, None
     with _on_device(keys):
-        _check(lib().srs_sort_soa_device(keys.numel(), kind, int(bool(up)),
-                                         int(cmp_sort_threshold), keys.data_ptr(), np_, pays,
-                                         sizes, kout, pout, _stream_ptr(stream, keys.device)))
+        _check(lib().srs_sort_soa_device_leaf(keys.numel(), kind, int(bool(up)),
+                                              int(cmp_sort_threshold), _leaf(cmp_sorter),
+                                              keys.data_ptr(), np_, pays, sizes, kout, pout,
+                                              _stream_ptr(stream, keys.device)))
 
 
 def sort_segments_device(keys, *payloads, bounds, up: bool = True, key_kind: int | None = None,
@@ -230,7 +250,8 @@ def sort_segments_device(keys, *payloads, bounds, up: bool = True, key_kind: int
 
 
 def sort_combined_device(elements, key_kind: int, up: bool = True,
-                         cmp_sort_threshold: int = 16, out=None, stream=None) -> None:
+                         cmp_sort_threshold: int = 16, out=None, stream=None,
+                         cmp_sorter: str = "insertion") -> None:
     """DataElement array on the device: `elements` is a contiguous (n, elem_size)
     uint8 tensor (or any contiguous tensor whose first dim is the record)."""
     if not (elements.is_cuda and elements.is_contiguous()):
@@ -242,10 +263,11 @@ def sort_combined_device(elements, key_kind: int, up: bool = True,
                 out.numel() * out.element_size() == elements.numel() * elements.element_size()):
             raise ValueError("out must be a contiguous tensor of the same bytes on the same GPU")
     with _on_device(elements):
-        _check(lib().srs_sort_aos_device(n, int(key_kind), int(bool(up)), int(cmp_sort_threshold),
-                                         elements.data_ptr(), esz,
-                                         None if out is None else out.data_ptr(),
-                                         _stream_ptr(stream, elements.device)))
+        _check(lib().srs_sort_aos_device_leaf(n, int(key_kind), int(bool(up)),
+                                              int(cmp_sort_threshold), _leaf(cmp_sorter),
+                                              elements.data_ptr(), esz,
+                                              None if out is None else out.data_ptr(),
+                                              _stream_ptr(stream, elements.device)))
 
 
 def fill_synthetic_device(keys, *payloads, seed: int = 42 << 32, first_index: int = 0,

@@ -21,6 +21,7 @@
 #include <vector>
 
 #include "simd_sort/radix_sort.hpp"
+#include "sort_method.hpp"  // own rewrite of the harness adapter's call shapes
 
 using namespace simd_sort;
 
@@ -140,10 +141,23 @@ static void test_case(Dist d, std::size_t n, unsigned seed) {
       if constexpr (sizeof...(Ps) > 0)
         std::apply([&](auto&... p) { std::tie(p[i]...) = e[i].payloads; }, pays);
     }
-  } else {
+  } else if (seed % 3 == 0) {
+    // the radixSort.hpp spelling (plain BitSorterSIMD), :1761-1768
     std::apply([&](auto&... p) {
       radix_sort::sort<Up, radix_sort::BitSorterSIMD, CmpSorterInsertionSort>(
           16, (SortIndex)n, keys.data(), p.data()...);
+    }, pays);
+  } else if (seed % 3 == 1) {
+    // the harness adapter's shape (src/sort_methods.hpp:77-97) with the
+    // src/radix_sort.hpp:109 spelling BitSorterSIMD<false>
+    std::apply([&](auto&... p) {
+      srs_test::RadixMethod<radix_sort::BitSorterSIMD<false>, CmpSorterInsertionSort>::
+          template sort<Up>((SortIndex)n, keys.data(), p.data()...);
+    }, pays);
+  } else {
+    // the defaulted thresholded form, radixSort.hpp:1761-1763
+    std::apply([&](auto&... p) {
+      radix_sort::sort<Up>(16, (SortIndex)n, keys.data(), p.data()...);
     }, pays);
   }
   std::string err;

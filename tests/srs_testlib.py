@@ -134,6 +134,10 @@ def ref_lib():
                                      ctypes.c_void_p, ctypes.c_void_p]
     lib.srs_ref_sort_aos.argtypes = [ctypes.c_int64, ctypes.c_int, ctypes.c_int,
                                      ctypes.c_int64, ctypes.c_void_p, ctypes.c_uint32]
+    lib.srs_ref_sort_soa_timed.argtypes = [ctypes.c_int64, ctypes.c_int, ctypes.c_int,
+                                           ctypes.c_int64, ctypes.c_void_p, ctypes.c_int32,
+                                           ctypes.c_void_p, ctypes.c_void_p,
+                                           ctypes.POINTER(ctypes.c_double)]
     return lib
 
 
@@ -141,6 +145,18 @@ def ref_sort_soa(kind, up, keys, payloads=(), thresh=16):
     rc = ref_lib().srs_ref_sort_soa(len(keys), kind, int(up), thresh, keys.ctypes.data,
                                     len(payloads), _ptrs(payloads), _sizes(payloads))
     assert rc == 0, rc
+
+
+def ref_sort_soa_timed(kind, up, keys, payloads=(), thresh=16):
+    """ref_sort_soa timed inside the library with CLOCK_PROCESS_CPUTIME_ID
+    around the sort call only (the reference's src/perf.hpp:33-46); returns
+    the CPU nanoseconds."""
+    ns = ctypes.c_double(0)
+    rc = ref_lib().srs_ref_sort_soa_timed(len(keys), kind, int(up), thresh, keys.ctypes.data,
+                                          len(payloads), _ptrs(payloads), _sizes(payloads),
+                                          ctypes.byref(ns))
+    assert rc == 0, rc
+    return ns.value
 
 
 def ref_sort_aos(kind, up, elems, thresh=16):

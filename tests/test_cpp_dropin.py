@@ -56,6 +56,50 @@ def test_dropin_accepts_every_reference_sorter_tag():
     assert r.returncode == 0, r.stderr.decode()[-2000:]
 
 
+def _compile_with(src, *extra):
+    return subprocess.run(["g++", "-std=c++17", "-Wall", "-Wextra", "-Werror", "-fsyntax-only",
+                           "-x", "c++", "-I", os.path.join(REPO, "include"), "-I", CPP, *extra,
+                           "-"], input=src.encode(), capture_output=True)
+
+
+def test_dropin_accepts_the_reference_call_forms():
+    """Every call spelling the reference accepts:
+    the defaulted thresholded form (radixSort.hpp:1761-1763), the plain
+    `BitSorterSIMD` of radixSort.hpp:1583 and the class template
+    `BitSorterSIMD<OneReg>` of src/radix_sort.hpp:109, and the harness
+    adapter's shapes (src/sort_methods.hpp:24-98, re-expressed in
+    tests/cpp/sort_method.hpp) for every bit/leaf sorter it names."""
+    src = ('#include "simd_sort/radix_sort.hpp"\n'
+           '#include "sort_method.hpp"\n'
+           "using namespace simd_sort; namespace rs = simd_sort::radix_sort;\n"
+           "using srs_test::RadixMethod;\n"
+           "int main(){ unsigned long long k[4]={3,1,2,0}; unsigned long long p[4]={0,1,2,3};\n"
+           " int i[4]={4,3,2,1}; double d[4]={1,2,3,4}; float f[4]={1,2,3,4};\n"
+           " rs::sort(16, 4, k, p); rs::sort<false>(16, 4, k); rs::sort(16, 4, f, p, i);\n"
+           " rs::sort<true, rs::BitSorterSIMD, CmpSorterInsertionSort>(16, 4, k, p);\n"
+           " rs::sort<true, rs::BitSorterSIMD<>, CmpSorterInsertionSort>(16, 4, k, p);\n"
+           " rs::sort<false, rs::BitSorterSIMD<true>, CmpSorterNoSort>(16, 4, k, p);\n"
+           " rs::sort<true, rs::BitSorterSequential>(64, 4, k, p);\n"
+           " rs::sort(4, k, p); rs::sort<false>(4, k);\n"
+           " DataElement<unsigned long long, unsigned long long> e[2]{};\n"
+           " rs::sort(16, 2, e); rs::sort(2, e); rs::sort<false>(2, e);\n"
+           " rs::sort<false, rs::BitSorterSIMD, CmpSorterNoSort>(16, 2, e);\n"
+           " rs::sort<true, rs::BitSorterSIMD<true>, CmpSorterInsertionSort>(16, 2, e);\n"
+           " static_assert(std::is_same_v<rs::BitSorterSIMD<>, rs::BitSorterSIMD<false>>);\n"
+           " (void)rs::BitSorterSIMD<true>::name(); (void)rs::BitSorterSequential::name();\n"
+           " RadixMethod<rs::BitSorterSIMD<false>, CmpSorterInsertionSort>::sort(4, k, p);\n"
+           " RadixMethod<rs::BitSorterSIMD<true>, CmpSorterInsertionSort>::sort<false>(4, k, p);\n"
+           " RadixMethod<rs::BitSorterSequential, CmpSorterInsertionSort>::sort(4, d);\n"
+           " RadixMethod<rs::BitSorterSIMD<false>, CmpSorterNoSort>::sortThresh(64, 4, k, p);\n"
+           " RadixMethod<rs::BitSorterSIMD<false>, CmpSorterBramasSmallSort>::sort(4, i, i);\n"
+           " RadixMethod<rs::BitSorterSIMD<true>, CmpSorterBramasSmallSort>::sort(4, d);\n"
+           " RadixMethod<rs::BitSorterSIMD<false>, CmpSorterInsertionSort, true>::sort(2, e);\n"
+           " return RadixMethod<rs::BitSorterSIMD<true>, CmpSorterNoSort, true>::name().size()"
+           " == 0; }\n")
+    r = _compile_with(src)
+    assert r.returncode == 0, r.stderr.decode()[-3000:]
+
+
 @pytest.mark.parametrize("call,msg", [
     ("radix_sort::sort<true, radix_sort::BitSorterSIMD, CmpSorterBramasSmallSort>(16, 4, f)",
      "only supports int and double"),
