@@ -1705,8 +1705,11 @@ __device__ __forceinline__ bool local_fast_body(const SortDesc* __restrict__ des
     // a bucket) and rank element-mapped with a masked loop; wider still goes
     // to the stable kernel.
     const bool wide = !exact && hi + 1 + IDXB > 64;
-    if (wide && sh - lo + IDXB > 64) {
-      bail();  // the stable kernel takes it
+    // (too wide for a rank word: the stable kernel takes it, unless the
+    // CmpSorterNoSort leaves need no rank, decided after the bucket pass)
+    const bool too_wide = wide && sh - lo + IDXB > 64;
+    if (too_wide && desc->leaf_skip == 0) {
+      bail();
       return true;
     }
     const uint64_t below = (sh - lo >= 64) ? ~0ull : ((1ull << (sh - lo)) - 1);
@@ -1823,7 +1826,7 @@ __device__ __forceinline__ bool local_fast_body(const SortDesc* __restrict__ des
     // recursion, all keys sharing the bits above sh) holds <= leaf_skip keys,
     // the buckets are the leaves and stay in bucket-pass order
     const bool skip_rank = maxlen <= desc->leaf_skip;
-    if (maxlen > kRankSortMax && !skip_rank) {
+    if ((maxlen > kRankSortMax || too_wide) && !skip_rank) {
       // a large bucket (duplicates or skew): local_stable_kernel takes the
       // segment (nothing has been written to global memory yet)
       bail();
