@@ -187,6 +187,20 @@ int srs_partition_device(int64_t num, int key_kind, int up, const void* keys,
                          void* keys_out, void* const* payloads_out,
                          int64_t* part_counts, void* stream);
 
+/* ---- host arrays over several GPUs --------------------------------------- */
+
+/* Devices the host-pointer entry points (srs_sort_soa, srs_sort_soa_leaf)
+ * may use. 0 devices (the default) = the calling thread's current device.
+ * With G > 1 devices a large SoA sort (>= 2^22 keys) splits the host array
+ * G ways: chunk g goes over device g's own PCIe link, the chunks are
+ * partitioned into G key ranges (a stable top-bits radix level), range h is
+ * gathered on device h over xGMI, sorted there and copied back to its place.
+ * The result is the same array a one-device sort gives. A device may be
+ * listed more than once (its shards then share it). The environment
+ * variable SRS_HOST_DEVICES ("all" or "0,1,2") sets the initial list. The
+ * reference sorts on one host thread and has no counterpart. */
+int srs_set_host_devices(int32_t num_devices, const int32_t* devices);
+
 /* ---- synthetic data (bench / tests) ------------------------------------- */
 
 /* keys[i] = splitmix64(seed + first_index + i) truncated/reinterpreted to the

@@ -21,6 +21,7 @@
 #include <map>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/srs_c_api.h"
@@ -214,12 +215,15 @@ struct Workspace {
   // srs_debug_last_fallbacks
   DevBuf small_taken;
   bool last_small = false;
+  // one call at a time per device (calls on different devices run in
+  // parallel: the multi-GPU host split sorts its shards from several threads)
+  std::mutex mu;
 };
 
-std::mutex g_wmu;
+std::mutex g_wmu;  // the map below
 std::map<int, Workspace*> g_ws;
 
-int get_ws(Workspace** out) {
+int get_ws_locked(Workspace** out) {
   int dev = 0;
   HIP_TRY(hipGetDevice(&dev));
   auto it = g_ws.find(dev);
@@ -235,9 +239,19 @@ int get_ws(Workspace** out) {
   return SRS_OK;
 }
 
+// The current device's workspace, locked for this call (lk holds W->mu).
+int acquire_ws(Workspace** out, std::unique_lock<std::mutex>* lk) {
+  {
+    std::lock_guard<std::mutex> g(g_wmu);
+    SRS_TRY(get_ws_locked(out));
+  }
+  *lk = std::unique_lock<std::mutex>((*out)->mu);
+  return SRS_OK;
+}
+
 size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
-// Holds the workspace for one call on stream `st` (under g_wmu): waits on the
+// Holds the workspace for one call on stream `st` (under W->mu): waits on the
 // device for the previous call's work on the workspace (any stream), and
 // marks the end of this call's work when it goes out of scope, also on error.
 struct WsUse {
@@ -1007,13 +1021,459 @@ bool whole_input_is_unsorted_leaf(const Request& R) {
 
 int sort_device(Request& R, hipStream_t st) {
   if (R.num <= 1 || whole_input_is_unsorted_leaf(R)) return copy_through(R, st);
-  std::lock_guard<std::mutex> lk(g_wmu);
   Workspace* W = nullptr;
-  SRS_TRY(get_ws(&W));
+  std::unique_lock<std::mutex> lk;
+  SRS_TRY(acquire_ws(&W, &lk));
   if (R.num <= kLocalCap) return run_small(W, R, st);  // touches no workspace data
   WsUse use;
   SRS_TRY(use.begin(W, st));
   return run_sort(W, R, st);
+}
+
+// ---------------------------------------------------------------------------
+// host arrays (the reference's calling convention, radixSort.hpp:1780):
+// staged PCIe copies, and the split of one host array over several GPUs
+// ---------------------------------------------------------------------------
+// PCIe on the MI355X box (tools/probe/host_copy.hip, 4 GB): pageable
+// hipMemcpy 55-56 GB/s H2D but 48-49 GB/s D2H (and 17 GB/s on a first
+// call); hipHostRegister costs ~19 GB/s, more than the copy it would speed
+// up; pinned DMA 57 GB/s both ways. Four host threads, each streaming its
+// stripe of a column through its own ring of pinned buffers (memcpy of one
+// chunk overlapping the DMA of the previous ones), reach 55.5 H2D / 54.7 D2H.
+constexpr int kStageThreads = 4;
+constexpr int kStageBufs = 3;
+constexpr size_t kStageChunk = size_t(32) << 20;
+constexpr size_t kStageMinBytes = size_t(16) << 20;  // below: one pageable hipMemcpy
+
+struct HostStage {  // per device, kept between calls
+  std::mutex mu;
+  int dev = 0;
+  char* pin[kStageThreads][kStageBufs] = {};
+  hipStream_t cst[kStageThreads] = {};  // copy streams (one per host thread)
+  hipEvent_t ev[kStageThreads][kStageBufs] = {};
+  hipStream_t st = nullptr;             // the sort's stream
+};
+std::mutex g_smu;
+std::map<int, HostStage*> g_stage;
+
+// (the calling thread's current device is `dev`)
+int get_stage(int dev, HostStage** out) {
+  std::lock_guard<std::mutex> g(g_smu);
+  auto it = g_stage.find(dev);
+  if (it != g_stage.end()) {
+    *out = it->second;
+    return SRS_OK;
+  }
+  HostStage* S = new HostStage();
+  S->dev = dev;
+  for (int t = 0; t < kStageThreads; t++) {
+    HIP_TRY(hipStreamCreateWithFlags(&S->cst[t], hipStreamNonBlocking));
+    for (int b = 0; b < kStageBufs; b++) {
+      HIP_TRY(hipHostMalloc((void**)&S->pin[t][b], kStageChunk, hipHostMallocDefault));
+      HIP_TRY(hipEventCreateWithFlags(&S->ev[t][b], hipEventDisableTiming));
+    }
+  }
+  HIP_TRY(hipStreamCreateWithFlags(&S->st, hipStreamNonBlocking));
+  g_stage[dev] = S;
+  *out = S;
+  return SRS_OK;
+}
+
+void release_host_stages() {
+  std::lock_guard<std::mutex> g(g_smu);
+  for (auto& kv : g_stage) {
+    HostStage* S = kv.second;
+    std::lock_guard<std::mutex> busy(S->mu);
+    for (int t = 0; t < kStageThreads; t++) {
+      (void)hipStreamSynchronize(S->cst[t]);
+      for (int b = 0; b < kStageBufs; b++) {
+        (void)hipHostFree(S->pin[t][b]);
+        (void)hipEventDestroy(S->ev[t][b]);
+      }
+      (void)hipStreamDestroy(S->cst[t]);
+    }
+    (void)hipStreamSynchronize(S->st);
+    (void)hipStreamDestroy(S->st);
+    delete S;
+  }
+  g_stage.clear();
+}
+
+// One thread's stripe [a, a + len) of a host <-> device copy through its ring.
+int stage_stripe(HostStage* S, int t, char* dptr, char* hptr, size_t len, bool h2d) {
+  HIP_TRY(hipSetDevice(S->dev));
+  const size_t m = (len + kStageChunk - 1) / kStageChunk;
+  hipStream_t cs = S->cst[t];
+  auto piece = [&](size_t i, size_t* off) {
+    *off = i * kStageChunk;
+    return std::min(kStageChunk, len - *off);
+  };
+  if (h2d) {
+    for (size_t i = 0; i < m; i++) {
+      size_t off;
+      const size_t n = piece(i, &off);
+      const int b = (int)(i % kStageBufs);
+      if (i >= (size_t)kStageBufs) HIP_TRY(hipEventSynchronize(S->ev[t][b]));  // its last DMA
+      memcpy(S->pin[t][b], hptr + off, n);
+      HIP_TRY(hipMemcpyAsync(dptr + off, S->pin[t][b], n, hipMemcpyHostToDevice, cs));
+      HIP_TRY(hipEventRecord(S->ev[t][b], cs));
+    }
+  } else {
+    for (size_t i = 0; i < m + kStageBufs; i++) {
+      if (i >= (size_t)kStageBufs) {  // drain chunk i - NB (its DMA went first)
+        size_t off;
+        const size_t j = i - kStageBufs, n = piece(j, &off);
+        const int b = (int)(j % kStageBufs);
+        HIP_TRY(hipEventSynchronize(S->ev[t][b]));
+        memcpy(hptr + off, S->pin[t][b], n);
+      }
+      if (i < m) {
+        size_t off;
+        const size_t n = piece(i, &off);
+        const int b = (int)(i % kStageBufs);
+        HIP_TRY(hipMemcpyAsync(S->pin[t][b], dptr + off, n, hipMemcpyDeviceToHost, cs));
+        HIP_TRY(hipEventRecord(S->ev[t][b], cs));
+      }
+    }
+  }
+  HIP_TRY(hipStreamSynchronize(cs));
+  return SRS_OK;
+}
+
+// A host <-> device copy of `bytes` (device S->dev; S->mu held by the caller).
+int staged_copy(HostStage* S, char* dptr, char* hptr, size_t bytes, bool h2d) {
+  if (bytes == 0) return SRS_OK;
+  if (bytes < kStageMinBytes) {
+    HIP_TRY(hipMemcpy(h2d ? (void*)dptr : (void*)hptr, h2d ? (void*)hptr : (void*)dptr, bytes,
+                      h2d ? hipMemcpyHostToDevice : hipMemcpyDeviceToHost));
+    return SRS_OK;
+  }
+  const size_t per = align_up((bytes + kStageThreads - 1) / kStageThreads, 4096);
+  int rc[kStageThreads];
+  std::string err[kStageThreads];
+  std::vector<std::thread> th;
+  for (int t = 0; t < kStageThreads; t++) {
+    rc[t] = SRS_OK;
+    const size_t a = std::min(bytes, per * t), e = std::min(bytes, per * (t + 1));
+    if (a >= e) continue;
+    th.emplace_back([&, t, a, e] {
+      rc[t] = stage_stripe(S, t, dptr + a, hptr + a, e - a, h2d);
+      if (rc[t] != SRS_OK) err[t] = g_err;  // (thread-local message)
+    });
+  }
+  for (auto& x : th) x.join();
+  for (int t = 0; t < kStageThreads; t++)
+    if (rc[t] != SRS_OK) return fail(rc[t], err[t]);
+  return SRS_OK;
+}
+
+// Restores the calling thread's current device on scope exit.
+struct DeviceGuard {
+  int dev = -1;
+  DeviceGuard() { (void)hipGetDevice(&dev); }
+  ~DeviceGuard() {
+    if (dev >= 0) (void)hipSetDevice(dev);
+  }
+};
+
+size_t col_width(const Request& R, int c) { return R.aos ? R.elem_size : R.widths[c]; }
+
+// One device: every column staged into HBM (W->stage), sorted there in
+// place, copied back.
+int host_sort_single(Request& R, int dev) {
+  DeviceGuard keep;
+  HIP_TRY(hipSetDevice(dev));
+  HostStage* S = nullptr;
+  SRS_TRY(get_stage(dev, &S));
+  std::lock_guard<std::mutex> slk(S->mu);
+  Workspace* W = nullptr;
+  std::unique_lock<std::mutex> lk;
+  SRS_TRY(acquire_ws(&W, &lk));
+  std::vector<size_t> off;
+  size_t total = 0;
+  for (int c = 0; c < R.ncols; c++) {
+    off.push_back(total);
+    total += align_up((size_t)R.num * col_width(R, c), 256);
+  }
+  hipStream_t st = S->st;
+  WsUse use;
+  SRS_TRY(use.begin(W, st));
+  HIP_TRY(hipStreamSynchronize(st));  // (the previous call's kernels may still read stage)
+  SRS_TRY(ensure(W->stage, total));
+  Request D = R;
+  for (int c = 0; c < R.ncols; c++) {
+    char* dp = (char*)W->stage.p + off[c];
+    SRS_TRY(staged_copy(S, dp, (char*)R.in_cols[c], (size_t)R.num * col_width(R, c), true));
+    D.in_cols[c] = D.out_cols[c] = dp;
+  }
+  SRS_TRY(run_sort(W, D, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  for (int c = 0; c < R.ncols; c++)
+    SRS_TRY(staged_copy(S, (char*)D.out_cols[c], (char*)R.out_cols[c],
+                        (size_t)R.num * col_width(R, c), false));
+  return SRS_OK;
+}
+
+// ---- one host array over several GPUs -------------------------------------
+// Shard g (device devs[g]) takes the g-th contiguous chunk of the host array
+// over its own PCIe link and histograms its top key bits; the host cuts the
+// bins into G key ranges of ~equal size; every shard partitions its chunk
+// into the G ranges (srs_partition_device's stable LUT scatter: the first
+// radix level); range h is gathered on its device, source shard by source
+// shard (xGMI peer copies), sorted there and copied back to its place in the
+// host array. Every byte crosses PCIe once each way, spread over G links.
+// The result is stable (partition and gather keep input order), so it is
+// the same array a one-GPU sort gives.
+constexpr int kSplitBits = 12;
+constexpr int64_t kSplitMinN = int64_t(1) << 22;
+
+std::mutex g_hdmu;
+std::vector<int> g_host_devs;  // srs_set_host_devices; empty = the current device
+bool g_host_devs_set = false;
+
+std::vector<int> host_devices() {
+  std::lock_guard<std::mutex> g(g_hdmu);
+  if (!g_host_devs_set) {
+    g_host_devs_set = true;
+    const char* e = getenv("SRS_HOST_DEVICES");  // "all" or "0,1,2,3"
+    if (e && *e) {
+      int ndev = 0;
+      if (!strcmp(e, "all")) {
+        if (hipGetDeviceCount(&ndev) == hipSuccess)
+          for (int d = 0; d < ndev; d++) g_host_devs.push_back(d);
+      } else {
+        for (const char* p = e; *p;) {
+          char* q = nullptr;
+          long v = strtol(p, &q, 10);
+          if (q == p) break;
+          g_host_devs.push_back((int)v);
+          p = *q == ',' ? q + 1 : q;
+        }
+      }
+    }
+  }
+  return g_host_devs;
+}
+
+struct ShardBufs {  // device buffers of one shard, kept between calls
+  int dev = 0;
+  DevBuf in, part, recv, hist, lut;
+};
+std::mutex g_shmu;
+std::vector<ShardBufs*> g_shards;
+
+ShardBufs* shard_bufs(int g, int dev) {
+  std::lock_guard<std::mutex> lk(g_shmu);
+  while ((int)g_shards.size() <= g) g_shards.push_back(new ShardBufs());
+  ShardBufs* B = g_shards[g];
+  if (B->dev != dev) {  // (another device list than last time)
+    DevBuf* bufs[] = {&B->in, &B->part, &B->recv, &B->hist, &B->lut};
+    for (DevBuf* b : bufs) {
+      if (b->p) (void)hipFree(b->p);
+      *b = DevBuf();
+    }
+    B->dev = dev;
+  }
+  return B;
+}
+
+// Runs f(g) for every shard in its own thread; the first failure wins.
+template <typename F>
+int for_shards(int G, F f) {
+  std::vector<int> rc(G, SRS_OK);
+  std::vector<std::string> err(G);
+  std::vector<std::thread> th;
+  for (int g = 0; g < G; g++)
+    th.emplace_back([&, g] {
+      rc[g] = f(g);
+      if (rc[g] != SRS_OK) err[g] = g_err;
+    });
+  for (auto& x : th) x.join();
+  for (int g = 0; g < G; g++)
+    if (rc[g] != SRS_OK) return fail(rc[g], err[g]);
+  return SRS_OK;
+}
+
+int host_sort_split(Request& R, const std::vector<int>& devs) {
+  const int G = (int)devs.size();
+  const int64_t n = R.num;
+  const int ks = key_size_of(R.kind);
+  const int bits = std::min(kSplitBits, 8 * ks);
+  const int nbins = 1 << bits;
+  SortDesc dm;
+  memset(&dm, 0, sizeof dm);
+  key_masks(R.kind, R.up, dm);
+  std::vector<int64_t> lo(G + 1);
+  for (int g = 0; g <= G; g++) lo[g] = n * g / G;
+  int64_t maxchunk = 0;
+  for (int g = 0; g < G; g++) maxchunk = std::max(maxchunk, lo[g + 1] - lo[g]);
+  std::vector<ShardBufs*> B(G);
+  std::vector<HostStage*> S(G);
+  for (int g = 0; g < G; g++) B[g] = shard_bufs(g, devs[g]);
+  std::vector<std::vector<uint64_t>> hist(G, std::vector<uint64_t>(nbins));
+
+  // A. H2D of every shard's chunk + its histogram
+  SRS_TRY(for_shards(G, [&](int g) -> int {
+    HIP_TRY(hipSetDevice(devs[g]));
+    SRS_TRY(get_stage(devs[g], &S[g]));
+    std::lock_guard<std::mutex> slk(S[g]->mu);
+    std::vector<size_t> off(R.ncols + 1);
+    size_t t = 0;
+    for (int c = 0; c < R.ncols; c++) {
+      off[c] = t;
+      t += align_up((size_t)maxchunk * R.widths[c], 256);
+    }
+    SRS_TRY(ensure(B[g]->in, t));
+    SRS_TRY(ensure(B[g]->part, t));
+    SRS_TRY(ensure(B[g]->hist, nbins * sizeof(uint64_t)));
+    const int64_t m = lo[g + 1] - lo[g];
+    for (int c = 0; c < R.ncols; c++)
+      SRS_TRY(staged_copy(S[g], (char*)B[g]->in.p + off[c],
+                          (char*)R.in_cols[c] + (size_t)lo[g] * R.widths[c],
+                          (size_t)m * R.widths[c], true));
+    hipStream_t st = S[g]->st;
+    HIP_TRY(hipMemsetAsync(B[g]->hist.p, 0, nbins * sizeof(uint64_t), st));
+    if (m > 0)
+      launch_key_hist(ks, m, B[g]->in.p, dm, bits, (unsigned long long*)B[g]->hist.p, st);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(hist[g].data(), B[g]->hist.p, nbins * sizeof(uint64_t),
+                           hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    return SRS_OK;
+  }));
+
+  // the bins -> G contiguous key ranges of ~n/G keys (bin b goes to range
+  // floor(G * (keys before b + half of b) / n), non-decreasing)
+  std::vector<int32_t> lut(nbins);
+  {
+    double before = 0;
+    int prev = 0;
+    for (int b = 0; b < nbins; b++) {
+      uint64_t hb = 0;
+      for (int g = 0; g < G; g++) hb += hist[g][b];
+      int r = (int)((before + 0.5 * (double)hb) * G / (double)n);
+      r = std::min(std::max(r, prev), G - 1);
+      lut[b] = prev = r;
+      before += (double)hb;
+    }
+  }
+
+  // B. every shard partitions its chunk into the G ranges
+  std::vector<std::vector<int64_t>> cnt(G, std::vector<int64_t>(G, 0));
+  SRS_TRY(for_shards(G, [&](int g) -> int {
+    HIP_TRY(hipSetDevice(devs[g]));
+    std::lock_guard<std::mutex> slk(S[g]->mu);
+    const int64_t m = lo[g + 1] - lo[g];
+    if (m == 0) return SRS_OK;
+    hipStream_t st = S[g]->st;
+    SRS_TRY(ensure(B[g]->lut, nbins * sizeof(int32_t)));
+    HIP_TRY(hipMemcpyAsync(B[g]->lut.p, lut.data(), nbins * sizeof(int32_t),
+                           hipMemcpyHostToDevice, st));
+    std::vector<size_t> off(R.ncols);
+    size_t t = 0;
+    for (int c = 0; c < R.ncols; c++) {
+      off[c] = t;
+      t += align_up((size_t)maxchunk * R.widths[c], 256);
+    }
+    Request P = R;
+    P.num = m;
+    for (int c = 0; c < R.ncols; c++) {
+      P.in_cols[c] = (char*)B[g]->in.p + off[c];
+      P.out_cols[c] = (char*)B[g]->part.p + off[c];
+    }
+    if (m == 1) {  // (run_partition needs two keys) the one key's range on the host
+      uint64_t kb = 0;
+      HIP_TRY(hipMemcpyAsync(&kb, P.in_cols[0], ks, hipMemcpyDeviceToHost, st));
+      HIP_TRY(hipStreamSynchronize(st));
+      const uint64_t u = kb ^ ((kb & dm.signbit) ? dm.mneg : dm.mpos);
+      cnt[g][lut[(u >> (8 * ks - bits)) & (nbins - 1)]] = 1;
+      for (int c = 0; c < R.ncols; c++)
+        HIP_TRY(hipMemcpyAsync(P.out_cols[c], P.in_cols[c], R.widths[c],
+                               hipMemcpyDeviceToDevice, st));
+      HIP_TRY(hipStreamSynchronize(st));
+      return SRS_OK;
+    }
+    Workspace* W = nullptr;
+    std::unique_lock<std::mutex> lk;
+    SRS_TRY(acquire_ws(&W, &lk));
+    WsUse use;
+    SRS_TRY(use.begin(W, st));
+    SRS_TRY(run_partition(W, P, bits, (const int32_t*)B[g]->lut.p, G, cnt[g].data(), st));
+    HIP_TRY(hipStreamSynchronize(st));
+    return SRS_OK;
+  }));
+
+  // C. range h gathered on its device (source-major: input order), sorted,
+  // copied back to its place in the host array
+  std::vector<int64_t> rtot(G, 0), rstart(G + 1, 0);
+  for (int h = 0; h < G; h++) {
+    for (int g = 0; g < G; g++) rtot[h] += cnt[g][h];
+    rstart[h + 1] = rstart[h] + rtot[h];
+  }
+  if (rstart[G] != n) return fail(SRS_ERR_INTERNAL, "host split: partition sizes do not add up");
+  for (int g = 0; g < G; g++)
+    for (int h = 0; h < G; h++)
+      if (devs[g] != devs[h]) {  // xGMI peer access (already enabled is fine)
+        HIP_TRY(hipSetDevice(devs[h]));
+        const hipError_t e = hipDeviceEnablePeerAccess(devs[g], 0);
+        if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) (void)hipGetLastError();
+      }
+  return for_shards(G, [&](int h) -> int {
+    HIP_TRY(hipSetDevice(devs[h]));
+    std::lock_guard<std::mutex> slk(S[h]->mu);
+    const int64_t m = rtot[h];
+    if (m == 0) return SRS_OK;
+    hipStream_t st = S[h]->st;
+    std::vector<size_t> roff(R.ncols), poff(R.ncols);
+    size_t t = 0, tp = 0;
+    for (int c = 0; c < R.ncols; c++) {
+      roff[c] = t;
+      t += align_up((size_t)m * R.widths[c], 256);
+      poff[c] = tp;
+      tp += align_up((size_t)maxchunk * R.widths[c], 256);
+    }
+    SRS_TRY(ensure(B[h]->recv, t));
+    Request D = R;
+    D.num = m;
+    D.thresh = R.leaf_mode == SRS_LEAF_UNSORTED ? R.thresh : 0;  // (no n <= thresh rule)
+    for (int c = 0; c < R.ncols; c++) D.in_cols[c] = D.out_cols[c] = (char*)B[h]->recv.p + roff[c];
+    int64_t at = 0;
+    for (int g = 0; g < G; g++) {
+      int64_t src = 0;  // range h's piece in shard g's partitioned chunk
+      for (int q = 0; q < h; q++) src += cnt[g][q];
+      const int64_t len = cnt[g][h];
+      for (int c = 0; c < R.ncols && len > 0; c++) {
+        const size_t w = R.widths[c];
+        char* dst = (char*)D.in_cols[c] + (size_t)at * w;
+        const char* from = (const char*)B[g]->part.p + poff[c] + (size_t)src * w;
+        if (devs[g] == devs[h])
+          HIP_TRY(hipMemcpyAsync(dst, from, (size_t)len * w, hipMemcpyDeviceToDevice, st));
+        else
+          HIP_TRY(hipMemcpyPeerAsync(dst, devs[h], from, devs[g], (size_t)len * w, st));
+      }
+      at += len;
+    }
+    {
+      Workspace* W = nullptr;
+      std::unique_lock<std::mutex> lk;
+      SRS_TRY(acquire_ws(&W, &lk));
+      if (m > 1 && !whole_input_is_unsorted_leaf(D)) {
+        if (m <= kLocalCap) {
+          SRS_TRY(run_small(W, D, st));
+        } else {
+          WsUse use;
+          SRS_TRY(use.begin(W, st));
+          SRS_TRY(run_sort(W, D, st));
+        }
+      }
+      HIP_TRY(hipStreamSynchronize(st));
+    }
+    for (int c = 0; c < R.ncols; c++)
+      SRS_TRY(staged_copy(S[h], (char*)D.out_cols[c],
+                          (char*)R.out_cols[c] + (size_t)rstart[h] * R.widths[c],
+                          (size_t)m * R.widths[c], false));
+    return SRS_OK;
+  });
 }
 
 int sort_host(Request& R) {
@@ -1021,36 +1481,18 @@ int sort_host(Request& R) {
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
     return fail(SRS_ERR_NO_DEVICE, "no HIP device available");
-  std::lock_guard<std::mutex> lk(g_wmu);
-  Workspace* W = nullptr;
-  SRS_TRY(get_ws(&W));
-  // stage every column in HBM (one allocation), sort in place there, copy back
-  std::vector<size_t> off;
-  size_t total = 0;
-  for (int c = 0; c < R.ncols; c++) {
-    off.push_back(total);
-    const size_t w = R.aos ? R.elem_size : R.widths[c];
-    total += align_up((size_t)R.num * w, 256);
+  const std::vector<int> devs = host_devices();
+  for (int d : devs)
+    if (d < 0 || d >= ndev) return fail(SRS_ERR_INVALID_ARG, "host device list: no such device");
+  // the split needs SoA columns, a size worth G PCIe links, and n > thresh
+  // (its shards are sub-ranges of one sort: no whole-input leaf rule)
+  if (devs.size() > 1 && !R.aos && R.num >= kSplitMinN && R.num > R.thresh) {
+    DeviceGuard keep;
+    return host_sort_split(R, devs);
   }
-  hipStream_t st = nullptr;
-  WsUse use;
-  SRS_TRY(use.begin(W, st));
-  SRS_TRY(ensure(W->stage, total));
-  Request D = R;
-  for (int c = 0; c < R.ncols; c++) {
-    const size_t w = R.aos ? R.elem_size : R.widths[c];
-    char* dp = (char*)W->stage.p + off[c];
-    HIP_TRY(hipMemcpy(dp, R.in_cols[c], (size_t)R.num * w, hipMemcpyHostToDevice));
-    D.in_cols[c] = D.out_cols[c] = dp;
-  }
-  SRS_TRY(run_sort(W, D, st));
-  for (int c = 0; c < R.ncols; c++) {
-    const size_t w = R.aos ? R.elem_size : R.widths[c];
-    HIP_TRY(hipMemcpy(R.out_cols[c], D.out_cols[c], (size_t)R.num * w,
-                      hipMemcpyDeviceToHost));
-  }
-  HIP_TRY(hipDeviceSynchronize());
-  return SRS_OK;
+  int dev = 0;
+  HIP_TRY(hipGetDevice(&dev));
+  return host_sort_single(R, devs.empty() ? dev : devs[0]);
 }
 
 int build_soa(Request& R, int64_t num, int kind, int up, int64_t thresh, void* keys,
@@ -1224,9 +1666,9 @@ int srs_sort_segments_device(int64_t num, int key_kind, int up, void* keys,
   R.seg_bounds = segment_bounds;
   R.nsegs = num_segments;
   R.known_top_bits = known_top_bits;
-  std::lock_guard<std::mutex> lk(g_wmu);
   Workspace* W = nullptr;
-  SRS_TRY(get_ws(&W));
+  std::unique_lock<std::mutex> lk;
+  SRS_TRY(acquire_ws(&W, &lk));
   WsUse use;
   SRS_TRY(use.begin(W, (hipStream_t)stream));
   return run_sort(W, R, (hipStream_t)stream);
@@ -1322,9 +1764,9 @@ int srs_partition_device(int64_t num, int key_kind, int up, const void* keys,
     part_counts[one] = 1;
     return copy_through(R, (hipStream_t)stream);
   }
-  std::lock_guard<std::mutex> lk(g_wmu);
   Workspace* W = nullptr;
-  SRS_TRY(get_ws(&W));
+  std::unique_lock<std::mutex> lk;
+  SRS_TRY(acquire_ws(&W, &lk));
   WsUse use;
   SRS_TRY(use.begin(W, (hipStream_t)stream));
   return run_partition(W, R, bits, part_of_bucket, num_parts, part_counts, (hipStream_t)stream);
@@ -1333,6 +1775,21 @@ int srs_partition_device(int64_t num, int key_kind, int up, const void* keys,
 const char* srs_last_error(void) { return g_err.c_str(); }
 
 const char* srs_version(void) { return "srs_amd 0.1.0 gfx950"; }
+
+int srs_set_host_devices(int32_t num_devices, const int32_t* devices) {
+  if (num_devices < 0 || num_devices > 512 || (num_devices > 0 && !devices))
+    return fail(SRS_ERR_INVALID_ARG, "num_devices must be in [0, 512] with a device array");
+  int ndev = 0;
+  if (num_devices > 0 && (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0))
+    return fail(SRS_ERR_NO_DEVICE, "no HIP device available");
+  for (int i = 0; i < num_devices; i++)
+    if (devices[i] < 0 || devices[i] >= ndev)
+      return fail(SRS_ERR_INVALID_ARG, "no such device in the host device list");
+  std::lock_guard<std::mutex> g(g_hdmu);
+  g_host_devs.assign(devices, devices + num_devices);
+  g_host_devs_set = true;
+  return SRS_OK;
+}
 
 int srs_set_kernel_timing(int enable) {
   std::lock_guard<std::mutex> lk(g_tmu);
@@ -1366,9 +1823,9 @@ int srs_debug_set_stamp_buffer(void* device_acc) {
 
 int srs_debug_last_fallbacks(int64_t* counts) {
   if (!counts) return fail(SRS_ERR_INVALID_ARG, "counts is NULL");
-  std::lock_guard<std::mutex> lk(g_wmu);
   Workspace* W = nullptr;
-  SRS_TRY(get_ws(&W));
+  std::unique_lock<std::mutex> lk;
+  SRS_TRY(acquire_ws(&W, &lk));
   counts[0] = counts[1] = 0;
   if (W->last_small) {
     HIP_TRY(hipDeviceSynchronize());
@@ -1385,9 +1842,21 @@ int srs_debug_last_fallbacks(int64_t* counts) {
 }
 
 int srs_release_workspace(void) {
+  release_host_stages();
+  {
+    std::lock_guard<std::mutex> g(g_shmu);
+    for (ShardBufs* B : g_shards) {
+      DevBuf* bufs[] = {&B->in, &B->part, &B->recv, &B->hist, &B->lut};
+      for (DevBuf* b : bufs)
+        if (b->p) (void)hipFree(b->p);
+      delete B;
+    }
+    g_shards.clear();
+  }
   std::lock_guard<std::mutex> lk(g_wmu);
   for (auto& kv : g_ws) {
     Workspace* w = kv.second;
+    { std::lock_guard<std::mutex> busy(w->mu); }  // no call is using it any more
     if (w->idle) {  // the last call's kernels may still read the buffers
       (void)hipEventSynchronize(w->idle);
       (void)hipEventDestroy(w->idle);

@@ -80,6 +80,7 @@ def lib() -> ctypes.CDLL:
     L.srs_partition_device.argtypes = [i64, ctypes.c_int, ctypes.c_int, vp, i32, vp, vp,
                                        ctypes.c_int, vp, i32, vp, vp, vp, vp]
     L.srs_debug_last_fallbacks.argtypes = [ctypes.POINTER(i64)]
+    L.srs_set_host_devices.argtypes = [i32, vp]
     L.srs_last_error.restype = ctypes.c_char_p
     L.srs_version.restype = ctypes.c_char_p
     L.srs_set_kernel_timing.argtypes = [ctypes.c_int]
@@ -139,6 +140,15 @@ def sort_thresh(cmp_sort_threshold: int, keys: np.ndarray, *payloads: np.ndarray
                                    int(cmp_sort_threshold), _leaf(cmp_sorter), keys.ctypes.data,
                                    len(payloads), _ptr_array([p.ctypes.data for p in payloads]),
                                    _size_array([p.dtype.itemsize for p in payloads])))
+
+
+def set_host_devices(devices=()) -> None:
+    """GPUs the host-array sorts may use (srs_set_host_devices): () = the
+    current device; [0, 1, ...] splits large host arrays over them (a device
+    may repeat)."""
+    d = [int(x) for x in devices]
+    arr = (ctypes.c_int32 * max(1, len(d)))(*d)
+    _check(lib().srs_set_host_devices(len(d), arr))
 
 
 def sort(keys: np.ndarray, *payloads: np.ndarray, up: bool = True) -> None:
