@@ -212,9 +212,12 @@ struct Workspace {
   hipEvent_t idle = nullptr;
   bool idle_pending = false;
   // single-launch small sorts (run_small): which fallback bodies ran, for
-  // srs_debug_last_fallbacks
-  DevBuf small_taken;
+  // srs_debug_last_fallbacks. One slot per stream: small sorts skip the
+  // workspace's stream-order wait, so sorts on different streams must not
+  // share a slot (the map is only touched under `mu`).
+  std::map<hipStream_t, DevBuf> small_taken;
   bool last_small = false;
+  hipStream_t last_small_stream = nullptr;
   // one call at a time per device (calls on different devices run in
   // parallel: the multi-GPU host split sorts its shards from several threads)
   std::mutex mu;
@@ -650,12 +653,14 @@ int run_small(Workspace* W, const Request& R, hipStream_t st) {
   set_columns(R, d, nullptr, nullptr, false, 0, nullptr, inplace);
   d.stamp_acc = g_stamp_acc;
   const Seg g{0, n, d.key_bits, inplace ? BUF_OUT : BUF_IN};
-  SRS_TRY(ensure(W->small_taken, 2 * sizeof(int64_t)));
+  DevBuf& taken = W->small_taken[st];
+  SRS_TRY(ensure(taken, 2 * sizeof(int64_t)));
   W->last_small = true;
+  W->last_small_stream = st;
   note_elems("local", (double)n);
   {
     TimedScope ts("local", (double)0, st);
-    launch_small_sort(ksl, d, g, (int64_t*)W->small_taken.p, st);
+    launch_small_sort(ksl, d, g, (int64_t*)taken.p, st);
   }
   HIP_TRY(hipGetLastError());
   return SRS_OK;
@@ -912,16 +917,14 @@ int run_sort(Workspace* W, const Request& R, hipStream_t st) {
     }
   }
   if (n_copy > 0) {
-    // the list stays on the device; only the longest length sizes the grid
-    // (a read-back the plain uniform case never pays: its copy list is empty)
-    std::vector<Seg> cp((size_t)n_copy);
-    HIP_TRY(hipMemcpyAsync(cp.data(), W->copy.p, n_copy * sizeof(Seg),
-                           hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipStreamSynchronize(st));
-    int64_t max_len = 0;
-    for (const Seg& g : cp) max_len = std::max<int64_t>(max_len, g.len);
+    // the list stays on the device (the level scratch arrays are free now)
+    SRS_TRY(ensure(W->tcount, n_copy * 8));
+    SRS_TRY(ensure(W->tbase, n_copy * 8));
+    SRS_TRY(ensure(W->scan_tmp, scan_temp_elems(n_copy) * 8));
     TimedScope ts("copy", (double)0, st);
-    launch_copy_list(d_desc, (const Seg*)W->copy.p, n_copy, max_len, st);
+    launch_copy_list(d_desc, (const Seg*)W->copy.p, n_copy, (uint64_t*)W->tcount.p,
+                     (uint64_t*)W->tbase.p, (uint64_t*)W->scan_tmp.p,
+                     (uint64_t*)W->totals.p + 2, st);
   }
   HIP_TRY(hipGetLastError());
   return SRS_OK;
@@ -932,6 +935,7 @@ int run_sort(Workspace* W, const Request& R, hipStream_t st) {
 // the caller's output arrays.
 int run_partition(Workspace* W, const Request& R, int bits, const int32_t* d_lut,
                   int nparts, int64_t* counts, hipStream_t st) {
+  W->last_small = false;  // (srs_debug_last_fallbacks then reports this call's counters)
   const int ks = key_size_of(R.kind);
   const int64_t n = R.num;
   SortDesc d;
@@ -1024,7 +1028,8 @@ int sort_device(Request& R, hipStream_t st) {
   Workspace* W = nullptr;
   std::unique_lock<std::mutex> lk;
   SRS_TRY(acquire_ws(&W, &lk));
-  if (R.num <= kLocalCap) return run_small(W, R, st);  // touches no workspace data
+  // (a small sort touches no workspace buffer but its stream's debug slot)
+  if (R.num <= kLocalCap) return run_small(W, R, st);
   WsUse use;
   SRS_TRY(use.begin(W, st));
   return run_sort(W, R, st);
@@ -1043,7 +1048,14 @@ int sort_device(Request& R, hipStream_t st) {
 constexpr int kStageThreads = 4;
 constexpr int kStageBufs = 3;
 constexpr size_t kStageChunk = size_t(32) << 20;
-constexpr size_t kStageMinBytes = size_t(16) << 20;  // below: one pageable hipMemcpy
+constexpr size_t kStageMinBytesDefault = size_t(16) << 20;  // below: one pageable hipMemcpy
+size_t stage_min_bytes() {  // (SRS_STAGE_MIN_MB overrides, for experiments)
+  static const size_t v = [] {
+    const char* e = getenv("SRS_STAGE_MIN_MB");
+    return e && *e ? (size_t)atoll(e) << 20 : kStageMinBytesDefault;
+  }();
+  return v;
+}
 
 struct HostStage {  // per device, kept between calls
   std::mutex mu;
@@ -1083,20 +1095,23 @@ void release_host_stages() {
   std::lock_guard<std::mutex> g(g_smu);
   for (auto& kv : g_stage) {
     HostStage* S = kv.second;
-    std::lock_guard<std::mutex> busy(S->mu);
+    { std::lock_guard<std::mutex> busy(S->mu); }  // no call is using it any more
     for (int t = 0; t < kStageThreads; t++) {
-      (void)hipStreamSynchronize(S->cst[t]);
+      if (S->cst[t]) (void)hipStreamSynchronize(S->cst[t]);
       for (int b = 0; b < kStageBufs; b++) {
-        (void)hipHostFree(S->pin[t][b]);
-        (void)hipEventDestroy(S->ev[t][b]);
+        if (S->pin[t][b]) (void)hipHostFree(S->pin[t][b]);
+        if (S->ev[t][b]) (void)hipEventDestroy(S->ev[t][b]);
       }
-      (void)hipStreamDestroy(S->cst[t]);
+      if (S->cst[t]) (void)hipStreamDestroy(S->cst[t]);
     }
-    (void)hipStreamSynchronize(S->st);
-    (void)hipStreamDestroy(S->st);
-    delete S;
+    if (S->st) {
+      (void)hipStreamSynchronize(S->st);
+      (void)hipStreamDestroy(S->st);
+    }
+    delete S;  // (after its lock is released: the lock lives inside S)
   }
   g_stage.clear();
+  (void)hipGetLastError();  // (nothing above may leave a sticky error behind)
 }
 
 // One thread's stripe [a, a + len) of a host <-> device copy through its ring.
@@ -1143,7 +1158,7 @@ int stage_stripe(HostStage* S, int t, char* dptr, char* hptr, size_t len, bool h
 // A host <-> device copy of `bytes` (device S->dev; S->mu held by the caller).
 int staged_copy(HostStage* S, char* dptr, char* hptr, size_t bytes, bool h2d) {
   if (bytes == 0) return SRS_OK;
-  if (bytes < kStageMinBytes) {
+  if (bytes < stage_min_bytes()) {
     HIP_TRY(hipMemcpy(h2d ? (void*)dptr : (void*)hptr, h2d ? (void*)hptr : (void*)dptr, bytes,
                       h2d ? hipMemcpyHostToDevice : hipMemcpyDeviceToHost));
     return SRS_OK;
@@ -1829,7 +1844,8 @@ int srs_debug_last_fallbacks(int64_t* counts) {
   counts[0] = counts[1] = 0;
   if (W->last_small) {
     HIP_TRY(hipDeviceSynchronize());
-    HIP_TRY(hipMemcpy(counts, W->small_taken.p, 2 * sizeof(int64_t), hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(counts, W->small_taken[W->last_small_stream].p, 2 * sizeof(int64_t),
+                      hipMemcpyDeviceToHost));
     return SRS_OK;
   }
   if (!W->ctr.p) return SRS_OK;
@@ -1864,16 +1880,19 @@ int srs_release_workspace(void) {
     DevBuf* bufs[] = {&w->tmp, &w->tmp2, &w->stage, &w->desc, &w->big[0], &w->big[1], &w->local, &w->local2, &w->fallback, &w->fallback2, &w->shist, &w->lut, &w->lut_rbits,
                       &w->copy, &w->plan, &w->tcount, &w->gcount, &w->tbase, &w->gbase,
                       &w->var, &w->sbase, &w->tile_seg, &w->group_seg, &w->hist, &w->offs,
-                      &w->gsum, &w->gofs, &w->scan_tmp, &w->totals, &w->ctr, &w->small_taken,
+                      &w->gsum, &w->gofs, &w->scan_tmp, &w->totals, &w->ctr,
                       &w->prun, &w->ptile, &w->btot, &w->bnt, &w->btile, &w->nt_over, &w->gtile,
                       &w->gorder};
     for (DevBuf* b : bufs)
       if (b->p) (void)hipFree(b->p);
+    for (auto& t : w->small_taken)
+      if (t.second.p) (void)hipFree(t.second.p);
     (void)hipHostFree(w->h_ctr);
     (void)hipHostFree(w->h_totals);
     delete w;
   }
   g_ws.clear();
+  (void)hipGetLastError();
   return SRS_OK;
 }
 

@@ -68,7 +68,9 @@ void launch_fill(int64_t n, int kind, uint64_t seed, uint64_t first, void* keys,
 void launch_set_desc(const SortDesc& d, SortDesc* out, hipStream_t st);
 // the copy list (finished segments not in OUT) home in one launch, column by
 // column with each buffer's stride (AoS slice columns back into records)
-void launch_copy_list(const SortDesc* d, const Seg* segs, int64_t nsegs, int64_t max_len,
-                      hipStream_t st);
+// (chunks / cbase: nsegs u64 each; scan_temp: scan_temp_elems(nsegs) u64;
+// total: one u64)
+void launch_copy_list(const SortDesc* d, const Seg* segs, int64_t nsegs, uint64_t* chunks,
+                      uint64_t* cbase, uint64_t* scan_temp, uint64_t* total, hipStream_t st);
 
 }  // namespace srs

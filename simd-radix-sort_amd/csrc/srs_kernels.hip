@@ -2888,37 +2888,59 @@ __device__ __forceinline__ void init_lists_body(Seg seg0, int to_local, Seg* big
 
 // Finished segments home: every segment of the copy list (finished, not in
 // OUT) is moved to OUT in one launch, column by column with each buffer's
-// stride. blockIdx.y picks the segment, blockIdx.x strides over it. (A
-// hipMemcpyAsync per segment and column cost ~5 us each: duplicate-heavy
-// inputs finish hundreds of large segments at once.)
+// stride. (A hipMemcpyAsync per segment and column cost ~5 us each:
+// duplicate-heavy inputs finish hundreds of large segments at once.) The
+// segments are cut into chunks of kCopyChunk records and a fixed grid walks
+// the chunks of all segments (a device prefix sum of chunk counts maps a
+// chunk to its segment), so a long segment among many short ones gets the
+// whole grid instead of its share of a per-segment split, and the list never
+// travels to the host.
+constexpr int kCopyChunk = 4096;
+constexpr int kCopyGrid = 2048;
+
+__global__ void copy_chunks_kernel(const Seg* __restrict__ segs, int64_t nsegs,
+                                   uint64_t* __restrict__ chunks) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < nsegs) chunks[i] = (uint64_t)((segs[i].len + kCopyChunk - 1) / kCopyChunk);
+}
+
 __global__ __launch_bounds__(256) void copy_list_kernel(const SortDesc* __restrict__ desc,
-                                                        const Seg* __restrict__ segs) {
-  const Seg g = segs[blockIdx.y];
+                                                        const Seg* __restrict__ segs,
+                                                        int64_t nsegs,
+                                                        const uint64_t* __restrict__ cbase,
+                                                        const uint64_t* __restrict__ total) {
+  const uint64_t nchunks = *total;
   const int ncols = desc->ncols;
-  for (int c = 0; c < ncols; c++) {
-    const Col& C = desc->cols[c];
-    const uint32_t si = C.stride[g.buf], so = C.stride[BUF_OUT];
-    const char* src = C.base[g.buf] + g.start * (int64_t)si;
-    char* dst = C.base[BUF_OUT] + g.start * (int64_t)so;
-    with_width(C.width, [&](auto W_) {
-      constexpr int W = decltype(W_)::value;
-      for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < g.len;
-           i += (int64_t)gridDim.x * 256)
-        stw<W>(dst + i * so, ldw<W>(src + i * si));
-    });
+  for (uint64_t w = blockIdx.x; w < nchunks; w += gridDim.x) {
+    // the segment holding chunk w: the last s with cbase[s] <= w
+    int64_t lo = 0, hi = nsegs - 1;
+    while (lo < hi) {
+      const int64_t mid = (lo + hi + 1) >> 1;
+      if (cbase[mid] <= w) lo = mid;
+      else hi = mid - 1;
+    }
+    const Seg g = segs[lo];
+    const int64_t first = (int64_t)(w - cbase[lo]) * kCopyChunk;
+    const int64_t cnt = min((int64_t)kCopyChunk, g.len - first);
+    for (int c = 0; c < ncols; c++) {
+      const Col& C = desc->cols[c];
+      const uint32_t si = C.stride[g.buf], so = C.stride[BUF_OUT];
+      const char* src = C.base[g.buf] + (g.start + first) * (int64_t)si;
+      char* dst = C.base[BUF_OUT] + (g.start + first) * (int64_t)so;
+      with_width(C.width, [&](auto W_) {
+        constexpr int W = decltype(W_)::value;
+        for (int64_t i = threadIdx.x; i < cnt; i += 256) stw<W>(dst + i * so, ldw<W>(src + i * si));
+      });
+    }
   }
 }
 
-void launch_copy_list(const SortDesc* d, const Seg* segs, int64_t nsegs, int64_t max_len,
-                      hipStream_t st) {
+void launch_copy_list(const SortDesc* d, const Seg* segs, int64_t nsegs, uint64_t* chunks,
+                      uint64_t* cbase, uint64_t* scan_temp, uint64_t* total, hipStream_t st) {
   if (nsegs <= 0) return;
-  // ~4096 blocks in all, at most one per 256 elements of the longest segment
-  const int64_t per = std::max<int64_t>(1, std::min<int64_t>((max_len + 255) / 256,
-                                                             (4096 + nsegs - 1) / nsegs));
-  for (int64_t s0 = 0; s0 < nsegs; s0 += 65535) {  // grid.y limit
-    const unsigned ny = (unsigned)std::min<int64_t>(65535, nsegs - s0);
-    copy_list_kernel<<<dim3((unsigned)per, ny), 256, 0, st>>>(d, segs + s0);
-  }
+  copy_chunks_kernel<<<(unsigned)((nsegs + 255) / 256), 256, 0, st>>>(segs, nsegs, chunks);
+  launch_excl_scan(chunks, cbase, nsegs, scan_temp, total, st);
+  copy_list_kernel<<<kCopyGrid, 256, 0, st>>>(d, segs, nsegs, cbase, total);
 }
 
 void launch_set_desc(const SortDesc& d, SortDesc* out, hipStream_t st) {

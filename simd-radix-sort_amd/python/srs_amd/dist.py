@@ -257,12 +257,16 @@ class ShardSorter:
         # 5: partition chunk by chunk; each chunk's round-0 messages go out
         # while the next chunk is partitioned
         pending = []
+        bad = False
         for c in range(C):
             a, b = cb[c], cb[c + 1]
             got = self.ops.partition(keys[a:b], [p[a:b] for p in pays], self.bits, group_of_bin,
                                      G, (self.part_keys[a:b], *[p[a:b] for p in self.part_pays]))
             if list(got) != mat[me][c]:
-                raise RuntimeError("partition sizes differ from the chunk histogram")
+                # earlier chunks' messages are already posted and the peers
+                # expect this chunk's: keep to the agreed message plan (the
+                # buffers are sized by it) and fail on every rank at the end
+                bad = True
             if self.stage_host:  # the staged send buffers take the partitioned chunk
                 for (sb, _), (msb, _) in zip(cols, mcols):
                     msb[a:b].copy_(sb[a:b])
@@ -296,6 +300,12 @@ class ShardSorter:
                     # needs no more levels than a group's would)
                     self.ops.sort_segments(rk, rps, [a, b], shared(gs))
         self.ops.finish(self.device)
+        # every rank learns whether any partition disagreed with the plan
+        flag = torch.tensor([1 if bad else 0], dtype=torch.int64, device=hist.device)
+        dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=self.group)
+        if int(flag.item()):
+            raise RuntimeError("partition sizes differ from the chunk histogram"
+                               + ("" if bad else " (on another rank)"))
         self.last_counts = (counts, [sum(mat[s][c][g] for c in range(C) for g in owned[me])
                                      for s in range(w)])
         return rk, rps

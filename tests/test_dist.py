@@ -180,3 +180,61 @@ def test_balanced_split_is_monotone_and_balanced():
         assert bool((p[1:] >= p[:-1]).all()) and int(p.min()) >= 0 and int(p.max()) < w
     u = balanced_split(torch.full((256,), 10, dtype=torch.int64), 8)
     assert torch.bincount(u.long(), minlength=8).tolist() == [32] * 8
+
+
+class _BadCountOps(NumpyShardOps):
+    """Reports wrong group sizes for the second partition chunk (after the
+    first chunk's messages are posted)."""
+
+    def __init__(self, kind):
+        super().__init__(kind)
+        self.calls = 0
+
+    def partition(self, *a, **k):
+        got = super().partition(*a, **k)
+        self.calls += 1
+        if self.calls == 2:
+            got = list(got)
+            got[0] += 1
+        return got
+
+
+def _bad_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "simd-radix-sort_amd",
+                                    "python"))
+    from srs_amd.dist import ShardSorter
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    rng = np.random.default_rng(rank)
+    n = 4000
+    keys = torch.from_numpy(rng.integers(0, 2**63, n, dtype=np.uint64))
+    pay = torch.arange(n, dtype=torch.int64)
+    ops = _BadCountOps(6) if rank == 0 else NumpyShardOps(6)
+    sorter = ShardSorter(ops, n, [torch.int64], keys.dtype, "cpu", bits=8, chunk_bytes=1024,
+                         chunks=3)
+    try:
+        sorter.sort(keys, [pay])
+        q.put((rank, "finished"))
+    except Exception as e:
+        q.put((rank, type(e).__name__ + ": " + str(e)[:200]))
+    dist.destroy_process_group()
+
+
+def test_shard_sort_failure_does_not_hang_peers():
+    """a rank that finds its partition sizes wrong after posting
+    messages keeps to the agreed message plan, so its peers are not left
+    waiting on receives, and every rank raises at the end."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bad_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    assert "partition sizes differ" in res[0], res
+    assert "partition sizes differ" in res[1] and "another rank" in res[1], res
+    for p in procs:
+        assert p.exitcode == 0

@@ -809,3 +809,26 @@ def test_float_zero_canon_large_threshold(dtype, n, up):
         ek, ep = stable_reference(kind, up, [keys, pay], thresh)
         assert bytes_equal(k, ek), (thresh, "keys")
         assert bytes_equal(p, ep), (thresh, "payload order")
+
+
+def test_copy_list_long_and_many_short_segments():
+    """Finished segments that are not in OUT go home through the copy list:
+    here one segment of 2^23 equal keys beside ~800 segments of 10000 equal
+    keys each (the chunked copy grid gives the long one the
+    whole grid), keys + two payload columns against torch's stable sort."""
+    torch = _torch()
+    n_long, n_short, reps = 1 << 23, 800, 10000
+    g = torch.Generator(device="cuda")
+    g.manual_seed(5)
+    short = torch.arange(1, n_short + 1, dtype=torch.int64, device="cuda").repeat_interleave(reps)
+    keys = torch.cat([torch.full((n_long,), 10**9, dtype=torch.int64, device="cuda"), short])
+    keys = keys[torch.randperm(keys.numel(), device="cuda", generator=g)]
+    n = keys.numel()
+    p1 = torch.arange(n, dtype=torch.int64, device="cuda")
+    p2 = (p1 & 0xFFFF).to(torch.int16)
+    outs = (torch.empty_like(keys), torch.empty_like(p1), torch.empty_like(p2))
+    srs_amd.sort_device(keys, p1, p2, out=outs)
+    ref_k, ref_i = torch.sort(keys, stable=True)
+    assert torch.equal(outs[0], ref_k)
+    assert torch.equal(outs[1], ref_i)
+    assert torch.equal(outs[2], (ref_i & 0xFFFF).to(torch.int16))
