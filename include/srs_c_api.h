@@ -235,6 +235,12 @@ int srs_kernel_stats(const char* name, int64_t* launches, double* total_ms,
  * local (16..31) kernels; NULL disables. No effect in the product build. */
 int srs_debug_set_stamp_buffer(void* device_acc);
 
+/* Diagnostic builds only (-DSRS_DIAG_LOOKBACK): the scatter also runs a
+ * decoupled look-back over its tiles and checks it against the count pass's
+ * offsets. status: >= ntiles * 512 uint32 of device memory; err: 4 uint64
+ * (mismatches, spin timeouts, look-back hops of digit 0). NULL disables. */
+int srs_debug_set_lookback(void* status, void* err);
+
 /* Segments the local-level fallback kernels took in the last sort on the
  * current device: counts[0] = handed to the stable kernel, counts[1] = handed
  * on to the LSD kernel. Synchronizes the device. Tests use it to prove that

@@ -36,6 +36,8 @@ static_assert(sizeof(SortDesc) <= 4096, "SortDesc is a kernel argument (start_ke
 
 thread_local std::string g_err = "no error";
 unsigned long long* g_stamp_acc = nullptr;  // srs_debug_set_stamp_buffer
+uint32_t* g_lb_status = nullptr;             // srs_debug_set_lookback
+unsigned long long* g_lb_err = nullptr;
 
 // SRS_TRACE_LEVELS=1: one stderr line per global level and per local stage
 // (segment counts; diagnostics only, costs one extra read-back per sort)
@@ -550,6 +552,8 @@ int run_level(Workspace* W, int ks, const SortDesc* d_desc, LevelState& S, int f
                    (Seg*)W->local2.p, (Seg*)W->copy.p, d_ctr, lut_rbits, st, M.mode,
                    (uint32_t*)W->prun.p);
   }
+  if (g_lb_status)  // (diagnostic look-back: fresh status words per level)
+    HIP_TRY(hipMemsetAsync(g_lb_status, 0, (size_t)ntiles * kMaxBins * 4, st));
   {
     TimedScope ts("scatter", (double)0, st);
     launch_scatter(ks, d_desc, plan, tile_seg, (uint64_t*)W->offs.p,
@@ -728,6 +732,8 @@ int run_sort(Workspace* W, const Request& R, hipStream_t st) {
   set_columns(R, d, tmp, tmp2, aos_cols, slice_bytes, tmp_off.data(), inplace, pair_cols);
 
   d.stamp_acc = g_stamp_acc;
+  d.lb_status = g_lb_status;
+  d.lb_err = g_lb_err;
   bool balanced = false, spread = false;
   int lut_entries = 0;
   SRS_TRY(plan_balanced_level(W, R, d, &balanced, &lut_entries, st, &spread));
@@ -1833,6 +1839,14 @@ int srs_kernel_stats(const char* name, int64_t* launches, double* total_ms, doub
 
 int srs_debug_set_stamp_buffer(void* device_acc) {
   g_stamp_acc = (unsigned long long*)device_acc;
+  return SRS_OK;
+}
+
+// (diagnostic builds, SRS_DIAG_LOOKBACK: status words of at least ntiles * 512
+// u32, zeroed by the caller before every level, and 4 u64 error counters)
+int srs_debug_set_lookback(void* status, void* err) {
+  g_lb_status = (uint32_t*)status;
+  g_lb_err = (unsigned long long*)err;
   return SRS_OK;
 }
 

@@ -65,6 +65,10 @@ struct SortDesc {
   int32_t lut_mode;   // 0 flat int32 table, 1 two-level u16 table (see DigitLut)
   int32_t lut_entries;  // mode 1: u16 entries (4096 + 16 per split bin)
   unsigned long long* stamp_acc;  // diagnostic builds only (SRS_STAMPS)
+  // diagnostic builds only (SRS_DIAG_LOOKBACK): per (tile, digit) look-back
+  // status words of the scatter and error counters [mismatch, timeout, hops]
+  uint32_t* lb_status;
+  unsigned long long* lb_err;
 };
 
 struct Seg {

@@ -1272,7 +1272,58 @@ struct TileInfo {
   int64_t base;   // first element of the tile
   int32_t cnt;    // elements in the tile (0: skip)
   int32_t s;      // segment
+  int64_t t;      // tile index in the level
 };
+
+#ifdef SRS_DIAG_LOOKBACK
+// Diagnostic: a decoupled look-back over the tiles of a
+// segment, per digit, as a one-pass scatter would need it instead of the
+// count pass + scans: publish the tile's digit count (flag 1), walk back
+// over the predecessors' words (flag 1: add and continue, flag 2: an
+// inclusive prefix, add and stop), publish the inclusive prefix (flag 2).
+// Status words are single 4-byte sc1 stores / sc1 loads (self-contained
+// {flag, value} granules). The result is only compared with the offsets
+// the count pass produced (lb_err[0] counts mismatches); spins are bounded.
+__device__ __forceinline__ void diag_lookback(const SortDesc* __restrict__ desc,
+                                              const SegPlan& P, int64_t t, uint32_t d,
+                                              uint32_t tb, int64_t my_off,
+                                              const uint64_t* __restrict__ offs,
+                                              const uint32_t* __restrict__ offs32) {
+  uint32_t* st = desc->lb_status;
+  const uint64_t first = offs32 ? offs32[P.tile_base * kMaxBins + d] : offs[P.tile_base * kMaxBins + d];
+  uint32_t pre = 0;
+  if (t == P.tile_base) {
+    __hip_atomic_store(&st[t * kMaxBins + d], (2u << 30) | tb, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  } else {
+    __hip_atomic_store(&st[t * kMaxBins + d], (1u << 30) | tb, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+    int64_t j = t - 1;
+    uint32_t spins = 0, hops = 0;
+    while (true) {
+      const uint32_t v = __hip_atomic_load(&st[j * kMaxBins + d], __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+      const uint32_t f = v >> 30;
+      if (f == 0) {
+        if (++spins > (1u << 22)) {
+          atomicAdd(&desc->lb_err[1], 1ull);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+        continue;
+      }
+      pre += v & 0x3FFFFFFFu;
+      hops++;
+      if (f == 2 || j == P.tile_base) break;
+      j--;
+    }
+    __hip_atomic_store(&st[t * kMaxBins + d], (2u << 30) | (pre + tb), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+    if (d == 0) atomicAdd(&desc->lb_err[2], (unsigned long long)hops);
+  }
+  if ((uint64_t)my_off - first != pre) atomicAdd(&desc->lb_err[0], 1ull);
+}
+#endif
 
 template <typename KT, typename U, bool PRE3>
 __device__ __forceinline__ TileInfo scatter_load_tile(
@@ -1283,6 +1334,7 @@ __device__ __forceinline__ TileInfo scatter_load_tile(
     uint64_t (&v2)[kScatterItems], int64_t& my_off) {
   constexpr int IT = kScatterItems;
   TileInfo ti;
+  ti.t = t;
   ti.s = tile_seg[t];
   const SegPlan P = plan[ti.s];
   if (gt) {  // gathered level (never skipped)
@@ -1318,7 +1370,8 @@ __device__ __forceinline__ void scatter_process_tile(
     const SortDesc* __restrict__ desc, const SegPlan* __restrict__ plan, ScatterLds<LUT>& L,
     const TileInfo& ti, int ncols, const uint64_t (&v0)[kScatterItems],
     uint64_t (&v1)[kScatterItems], uint64_t (&v2)[kScatterItems], int64_t my_off,
-    const DigitLut& lut) {
+    const DigitLut& lut, const uint64_t* __restrict__ lb_offs = nullptr,
+    const uint32_t* __restrict__ lb_offs32 = nullptr) {
   constexpr int NT = kScatterThreads;
   constexpr int IT = kScatterItems;
   constexpr int NW = NT / 64;
@@ -1374,6 +1427,10 @@ __device__ __forceinline__ void scatter_process_tile(
       L.bin_start[my_bin] = ex;
       L.gdst[my_bin] = P.start + my_off - (int64_t)ex;
     }
+#ifdef SRS_DIAG_LOOKBACK
+    if (my_bin < nb && desc->lb_status)
+      diag_lookback(desc, P, ti.t, my_bin, tb, my_off, lb_offs, lb_offs32);
+#endif
   }
   lds_barrier();
   STAMP();  // 3: tile scan
@@ -1520,7 +1577,8 @@ __global__ __launch_bounds__(kScatterThreads, SRS_SCATTER_WAVES_PER_EU) void sca
   if (ti.cnt == 0) return;
   // (the table is published by the barrier at the top of the tile)
   const DigitLut lut = stage_lut<LUT, kScatterThreads>(desc, slut);
-  scatter_process_tile<KT, U, LUT, CZ, PRE3>(desc, plan, L, ti, ncols, v0, v1, v2, my_off, lut);
+  scatter_process_tile<KT, U, LUT, CZ, PRE3>(desc, plan, L, ti, ncols, v0, v1, v2, my_off, lut,
+                                             offs, offs32);
 }
 
 // ---------------------------------------------------------------------------
