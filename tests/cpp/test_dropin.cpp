@@ -237,9 +237,63 @@ static void all_types(std::size_t n, unsigned seed) {  // src/test.cpp:155-169
   all_payloads<Combined, Up, double>(n, seed);
 }
 
+// CmpSorterNoSort through the header (src/cmp_sorters.hpp:66-78): leaves of
+// <= thresh elements stay in partition order, so the output splits into
+// consecutive runs of <= thresh elements, each holding exactly the keys a
+// full sort puts there, and the payloads stay with their keys.
+template <typename K>
+static bool nosort_case(std::size_t n, SortIndex thresh, unsigned seed) {
+  std::mt19937 gen(seed);
+  std::vector<K> keys = make_keys<K>(n, Dist::Uniform, gen);
+  const std::vector<K> orig = keys;
+  std::vector<uint64_t> pay(n);
+  for (std::size_t i = 0; i < n; i++) pay[i] = payload_of<K, uint64_t>(keys[i], 0);
+  srs_test::RadixMethod<radix_sort::BitSorterSIMD<false>, CmpSorterNoSort>::sortThresh(
+      thresh, (SortIndex)n, keys.data(), pay.data());
+  std::vector<K> sorted = orig;
+  std::sort(sorted.begin(), sorted.end());
+  // leaf boundaries: every key before a cut is <= every key after it
+  std::vector<K> suffix_min(n + 1);
+  for (std::size_t i = n; i-- > 0;) suffix_min[i] = i + 1 < n ? std::min(keys[i], suffix_min[i + 1]) : keys[i];
+  K prefix_max = keys[0];
+  std::size_t last_cut = 0;
+  bool ok = same_key_multiset(keys, orig), unsorted = false;
+  for (std::size_t i = 1; i <= n && ok; i++) {
+    if (i < n) unsorted |= keys[i] < keys[i - 1];
+    if (i == n || !(suffix_min[i] < prefix_max)) {  // a cut before i
+      ok &= (SortIndex)(i - last_cut) <= thresh;
+      last_cut = i;
+    }
+    if (i < n) prefix_max = std::max(prefix_max, keys[i]);
+  }
+  for (std::size_t i = 0; i < n && ok; i++) ok &= pay[i] == payload_of<K, uint64_t>(keys[i], 0);
+  // (n > thresh and uniform integer keys: some leaf must be left unsorted;
+  // uniform floats put half a segment under one exponent, a bucket the local
+  // pass must rank, so their leaves may all come back sorted, which also
+  // meets the guarantee)
+  if constexpr (std::is_integral_v<K>) ok &= unsorted || n <= (std::size_t)thresh;
+  g_cases++;
+  if (!ok) {
+    g_failed++;
+    std::printf("Testing: %s, CmpSorterNoSort, thresh %ld, n=%zu: FAILED\n", tname<K>(),
+                (long)thresh, n);
+  }
+  return ok;
+}
+
 int main(int argc, char** argv) {
   const std::size_t max_num = argc > 1 ? std::stoul(argv[1]) : 100000;
   const unsigned seed = argc > 2 ? (unsigned)std::stoul(argv[2]) : 42u;
+  {
+    const long before = g_failed;
+    for (std::size_t n : {10000ul, 300000ul})
+      for (SortIndex t : {16, 64}) {
+        nosort_case<uint64_t>(n, t, seed);
+        nosort_case<int32_t>(n, t, seed + 1);
+        nosort_case<double>(n, t, seed + 2);
+      }
+    std::printf("Testing CmpSorterNoSort leaves: %s\n", g_failed == before ? "passed" : "FAILED");
+  }
   for (std::size_t n = 1; n <= max_num; n *= 10) {
     const long before = g_failed;
     all_types<false, true>(n, seed);

@@ -24,7 +24,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, dist_kind, kind, q):
+def _worker(rank, world, port, dist_kind, kind, q, n_base=200_000):
     try:
         os.environ["MASTER_ADDR"] = "127.0.0.1"
         os.environ["MASTER_PORT"] = str(port)
@@ -35,10 +35,15 @@ def _worker(rank, world, port, dist_kind, kind, q):
         from srs_amd.dist import HipShardOps, ShardSorter
         torch.cuda.set_device(0)
         dist.init_process_group("gloo", rank=rank, world_size=world)
-        n = 200_000 + 3_001 * rank  # ragged shards
+        n = n_base + 3_001 * rank  # ragged shards
         g = torch.Generator(device="cuda")
         g.manual_seed(1000 + rank)
-        if dist_kind == "uniform":
+        pay = torch.arange(n, dtype=torch.int64, device="cuda") + rank * 10**7
+        if dist_kind == "c4":  # BASELINE C4's generator: global indices [r * n, (r + 1) * n)
+            keys = torch.empty(n, dtype=torch.int64, device="cuda")
+            srs_amd.fill_synthetic_device(keys, pay, seed=42 << 32, first_index=rank * n_base,
+                                          key_kind=kind)
+        elif dist_kind == "uniform":
             keys = torch.randint(-2**63, 2**63 - 1, (n,), dtype=torch.int64, device="cuda",
                                  generator=g)
         elif dist_kind == "skewed":  # a few top buckets + duplicates
@@ -48,7 +53,6 @@ def _worker(rank, world, port, dist_kind, kind, q):
             keys = torch.full((n,), 77, dtype=torch.int64, device="cuda")
         else:  # floats
             keys = torch.randn(n, device="cuda", generator=g)
-        pay = torch.arange(n, dtype=torch.int64, device="cuda") + rank * 10**7
         sorter = ShardSorter(HipShardOps(kind), n, [torch.int64], keys.dtype, "cuda",
                              chunk_bytes=64 << 10, stage_host=True)
         for _ in range(2):  # twice: buffers are reused
@@ -72,9 +76,12 @@ def _transformed(k, kind):
     return transformed_keys(kind, True, k)
 
 
-@pytest.mark.parametrize("world,dist_kind,kind", [
-    (2, "uniform", 7), (3, "skewed", 7), (4, "uniform", 7), (3, "equal", 7), (2, "float", 8)])
-def test_shard_sorter_multi_rank_on_gpu(world, dist_kind, kind):
+@pytest.mark.parametrize("world,dist_kind,kind,n_base", [
+    (2, "uniform", 7, 200_000), (3, "skewed", 7, 200_000), (4, "uniform", 7, 200_000),
+    (3, "equal", 7, 200_000), (2, "float", 8, 200_000),
+    # C4's shape (u64 key + f(key) payload from global indices) at 8 ranks
+    (8, "c4", 6, 1_000_000)])
+def test_shard_sorter_multi_rank_on_gpu(world, dist_kind, kind, n_base):
     torch = pytest.importorskip("torch")
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
@@ -82,7 +89,7 @@ def test_shard_sorter_multi_rank_on_gpu(world, dist_kind, kind):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, dist_kind, kind, q))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, dist_kind, kind, q, n_base))
              for r in range(world)]
     for p in procs:
         p.start()
