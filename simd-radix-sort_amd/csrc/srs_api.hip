@@ -893,8 +893,11 @@ int run_sort(Workspace* W, const Request& R, hipStream_t st) {
     unsigned long long* nfb2 = &d_ctr->n_fallback2;
     {
       TimedScope ts1("local_fast", 0, st);
-      if (n_local2 > 0) launch_local(ksl, d_desc, (Seg*)W->local2.p, n_local2, 1, fb, nfb, st);
-      if (n_local > 0) launch_local(ksl, d_desc, (Seg*)W->local.p, n_local, 0, fb1, nfb1, st);
+      const bool rec16 = aos_cols && R.elem_size == 16;
+      if (n_local2 > 0)
+        launch_local(ksl, d_desc, (Seg*)W->local2.p, n_local2, 1, fb, nfb, st, rec16);
+      if (n_local > 0)
+        launch_local(ksl, d_desc, (Seg*)W->local.p, n_local, 0, fb1, nfb1, st, rec16);
     }
     {
       TimedScope ts2("local_stable", 0, st);

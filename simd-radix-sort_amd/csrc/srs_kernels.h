@@ -50,8 +50,11 @@ void launch_stripe_tables(const uint32_t* prun, int64_t nstripes, int nb, uint32
                           int64_t tiles_cap = 0);  // torder: tiles_cap entries + nstripes of scratch
 void launch_key_hist(int key_size, int64_t n, const void* keys, const SortDesc& d, int bits,
                      unsigned long long* hist, hipStream_t st);
+// rec16: AoS records of 16 bytes held as two slice columns in TMP / TMP2
+// (the local pass then writes whole records, one 16-byte store each)
 void launch_local(int key_size, const SortDesc* d, const Seg* segs, int64_t nsegs, int big_class,
-                  Seg* fallback, unsigned long long* fallback_count, hipStream_t st);
+                  Seg* fallback, unsigned long long* fallback_count, hipStream_t st,
+                  bool rec16 = false);
 void launch_local_stable(int key_size, const SortDesc* d, const Seg* segs,
                          const unsigned long long* nsegs, int big_class, Seg* fallback,
                          unsigned long long* fallback_count, int grid, hipStream_t st);

@@ -1686,7 +1686,7 @@ struct FastLds {
 // then); block-uniform.
 // bail() runs (every thread) right where the segment is handed over: the
 // grid kernel appends it to its fallback list there.
-template <typename KT, typename U, int NT, int IT, bool CZ, typename Bail>
+template <typename KT, typename U, int NT, int IT, bool CZ, bool REC16 = false, typename Bail>
 __device__ __forceinline__ bool local_fast_body(const SortDesc* __restrict__ desc, const Seg g,
                                                 FastLds<NT, IT>& Ls, Bail bail) {
   constexpr int NW = NT / 64;
@@ -2085,6 +2085,50 @@ __device__ __forceinline__ bool local_fast_body(const SortDesc* __restrict__ des
     for (int k = 0; k < IT; k++) perm[ebase + k * 64] = (uint16_t)(ebase + k * 64);
     lds_barrier();
   }
+  // ---- 4'. 16-byte records (AoS records of 16 bytes that travelled as two
+  // dense 8-byte slice columns through TMP / TMP2, C3): both slices staged in
+  // turn, each output slot's key slice held in registers across the second
+  // staging, then one 16-byte store per record instead of two 8-byte stores
+  // at stride 16 into half-written lines.
+  // (an instantiation of its own, REC16: the extra path measurably slowed
+  // C1's kernel, 6.43 -> 6.51 ms, when compiled into it)
+  if (REC16 && ncols == 2 && desc->tmp2 && !desc->pair &&
+      (g.buf == BUF_TMP || g.buf == BUF_TMP2) &&
+      desc->cols[0].width == 8 && desc->cols[1].width == 8 &&
+      desc->cols[0].stride[BUF_OUT] == 16 && desc->cols[1].stride[BUF_OUT] == 16 &&
+      desc->cols[1].base[BUF_OUT] == desc->cols[0].base[BUF_OUT] + 8) {
+    load_strip<IT, true, 8>(vn, desc->cols[1].base[g.buf], 8, 8, base, ebase, cnt);
+#pragma unroll
+    for (int k = 0; k < IT; k++)
+      if (valid(k)) sbuf[ebase + k * 64] = v0[k];
+    lds_barrier();
+    uint64_t ko[IT];
+#pragma unroll
+    for (int k = 0; k < IT; k++) ko[k] = sbuf[valid(k) ? perm[ebase + k * 64] : 0];
+    lds_barrier();
+#pragma unroll
+    for (int k = 0; k < IT; k++)
+      if (valid(k)) sbuf[ebase + k * 64] = vn[k];
+    lds_barrier();
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    const __amdgpu_buffer_rsrc_t r = strip_rsrc(desc->cols[0].base[BUF_OUT] + base * 16,
+                                                cnt > 0 ? (uint32_t)cnt * 16u : 0u);
+#pragma unroll
+    for (int k = 0; k < IT; k++) {
+      const uint64_t pv = sbuf[valid(k) ? perm[ebase + k * 64] : 0];
+      u32x4 x;
+      x[0] = (uint32_t)ko[k];
+      x[1] = (uint32_t)(ko[k] >> 32);
+      x[2] = (uint32_t)pv;
+      x[3] = (uint32_t)(pv >> 32);
+      __builtin_amdgcn_raw_buffer_store_b128(x, r, (uint32_t)(ebase + k * 64) * 16u, 0, 0);
+    }
+    STAMP();
+    STAMP();
+    STAMP_FLUSH(1);
+    return false;
+  }
+
   // output slot e takes input element perm[e]
   uint32_t id[IT];
 #pragma unroll
@@ -2139,14 +2183,14 @@ __device__ __forceinline__ bool local_fast_body(const SortDesc* __restrict__ des
   return false;
 }
 
-template <typename KT, typename U, int NT, int IT, int WPE, bool CZ>
+template <typename KT, typename U, int NT, int IT, int WPE, bool CZ, bool REC16 = false>
 __global__ __launch_bounds__(NT, WPE) void local_kernel(const SortDesc* __restrict__ desc,
                                                    const Seg* __restrict__ segs,
                                                    Seg* __restrict__ fallback,
                                                    unsigned long long* fallback_count) {
   __shared__ FastLds<NT, IT> Ls;
   const Seg g = segs[blockIdx.x];
-  local_fast_body<KT, U, NT, IT, CZ>(desc, g, Ls, [&] {
+  local_fast_body<KT, U, NT, IT, CZ, REC16>(desc, g, Ls, [&] {
     if (threadIdx.x == 0) fallback[atomicAdd(fallback_count, 1ull)] = g;
   });
 }
@@ -2840,16 +2884,20 @@ void launch_stripe_tables(const uint32_t* prun, int64_t nstripes, int nb, uint32
 }
 
 void launch_local(int key_size, const SortDesc* d, const Seg* segs, int64_t nsegs, int big_class,
-                  Seg* fallback, unsigned long long* fallback_count, hipStream_t st) {
-#define CALL(KT, U, CZ)                                                                  \
-  if (big_class)                                                                         \
-    local_kernel<KT, U, kLocalThreads, kLocalItems, kLocalWavesPerEU, CZ>                \
-        <<<(unsigned)nsegs, kLocalThreads, 0, st>>>(d, segs, fallback, fallback_count);  \
-  else                                                                                   \
-    local_kernel<KT, U, kLocalThreadsSmall, kLocalItemsSmall, kLocalWavesPerEUSmall, CZ> \
+                  Seg* fallback, unsigned long long* fallback_count, hipStream_t st,
+                  bool rec16) {
+#define CALL_R(KT, U, CZ, R)                                                                \
+  if (big_class)                                                                            \
+    local_kernel<KT, U, kLocalThreads, kLocalItems, kLocalWavesPerEU, CZ, R>                \
+        <<<(unsigned)nsegs, kLocalThreads, 0, st>>>(d, segs, fallback, fallback_count);     \
+  else                                                                                      \
+    local_kernel<KT, U, kLocalThreadsSmall, kLocalItemsSmall, kLocalWavesPerEUSmall, CZ, R> \
         <<<(unsigned)nsegs, kLocalThreadsSmall, 0, st>>>(d, segs, fallback, fallback_count)
+#define CALL(KT, U, CZ) \
+  if (rec16) { CALL_R(KT, U, CZ, true); } else { CALL_R(KT, U, CZ, false); }
   SRS_KEY_DISPATCH(key_size, CALL)
 #undef CALL
+#undef CALL_R
 }
 
 void launch_local_stable(int key_size, const SortDesc* d, const Seg* segs,
