@@ -36,14 +36,31 @@ template <> struct UIntOf<2> { using type = uint16_t; };
 template <> struct UIntOf<4> { using type = uint32_t; };
 template <> struct UIntOf<8> { using type = uint64_t; };
 
+// The reference's CmpSorterNoSort (src/cmp_sorters.hpp:66-78) lives outside
+// the single header; a leaf sorter is only a type with a static
+// sort<Up>(left, right, keys, payloads...) that radixRecursion calls on each
+// range of <= cmpSortThreshold elements (radixSort.hpp:1743). This one leaves
+// the range as the partitions left it, as the reference's does.
+struct LeafUnsorted {
+  template <bool Up, typename K, typename... Ps>
+  static inline void sort(const SortIndex, const SortIndex, K* const, Ps* const...) {}
+};
+
+// leaf: 0 = CmpSorterInsertionSort, 1 = the no-op leaf (SRS_LEAF_UNSORTED)
+thread_local int g_leaf = 0;
+
 template <typename K, bool Up, std::size_t... Sz, std::size_t... I>
 int sort_soa_seq(int64_t thresh, int64_t num, void* keys, void* const* pays,
                  std::index_sequence<I...>) {
   // radix_sort::sort<Up, BitSorterSIMD, CmpSorterInsertionSort>(thresh, ...)
   // radixSort.hpp:1761-1768 (the two-argument sort() uses thresh = 16).
-  rs::sort<Up, rs::BitSorterSIMD, simd_sort::CmpSorterInsertionSort>(
-      (SortIndex)thresh, (SortIndex)num, (K*)keys,
-      ((typename UIntOf<Sz>::type*)pays[I])...);
+  if (g_leaf == 1)
+    rs::sort<Up, rs::BitSorterSIMD, LeafUnsorted>((SortIndex)thresh, (SortIndex)num, (K*)keys,
+                                                  ((typename UIntOf<Sz>::type*)pays[I])...);
+  else
+    rs::sort<Up, rs::BitSorterSIMD, simd_sort::CmpSorterInsertionSort>(
+        (SortIndex)thresh, (SortIndex)num, (K*)keys,
+        ((typename UIntOf<Sz>::type*)pays[I])...);
   return 0;
 }
 
@@ -154,6 +171,20 @@ int srs_ref_sort_soa_timed(int64_t num, int kind, int up, int64_t thresh, void* 
   const int rc = srs_ref_sort_soa(num, kind, up, thresh, keys, np, pays, sz);
   clock_gettime(CLOCK_PROCESS_CPUTIME_ID, &b);
   if (cpu_ns) *cpu_ns = (b.tv_sec - a.tv_sec) * 1e9 + (double)(b.tv_nsec - a.tv_nsec);
+  return rc;
+}
+
+// srs_ref_sort_soa_timed with the leaf sorter chosen at run time (leaf as
+// srs_sort_soa_leaf's: 0 insertion sort, 1 leaves unsorted, the reference's
+// CmpSorterNoSort); used by tools/perf_dat.py's cmpThresh files
+// (src/perf.hpp:159-212).
+int srs_ref_sort_soa_leaf_timed(int64_t num, int kind, int up, int64_t thresh, int leaf,
+                                void* keys, int32_t np, void* const* pays, const uint32_t* sz,
+                                double* cpu_ns) {
+  if (leaf != 0 && leaf != 1) return -3;
+  g_leaf = leaf;
+  const int rc = srs_ref_sort_soa_timed(num, kind, up, thresh, keys, np, pays, sz, cpu_ns);
+  g_leaf = 0;
   return rc;
 }
 

@@ -138,6 +138,10 @@ def ref_lib():
                                            ctypes.c_int64, ctypes.c_void_p, ctypes.c_int32,
                                            ctypes.c_void_p, ctypes.c_void_p,
                                            ctypes.POINTER(ctypes.c_double)]
+    lib.srs_ref_sort_soa_leaf_timed.argtypes = [
+        ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int64, ctypes.c_int,
+        ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p,
+        ctypes.POINTER(ctypes.c_double)]
     return lib
 
 

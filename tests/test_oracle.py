@@ -110,6 +110,42 @@ def test_oracle_vs_reference_combined(esz):
     assert beq(a, b)
 
 
+@needs_ref
+@pytest.mark.parametrize("thresh", [1, 16, 64, 1024])
+def test_reference_leaves_unsorted_guarantee(thresh):
+    """The reference with its no-op leaf sorter (CmpSorterNoSort,
+    src/cmp_sorters.hpp:66-78; oracle/_ref's leaf = 1) keeps the contract
+    tests/test_gpu_leaf.py holds the GPU's SRS_LEAF_UNSORTED mode to: the
+    multiset is kept and every key ends within thresh - 1 places of its
+    sorted slot (thesis 3113-3124). Sorted leaves (leaf = 0) give the
+    insertion sort's fully sorted output."""
+    import ctypes
+    lib = ref_lib()
+    rng = np.random.default_rng(thresh)
+    n = 1 << 16
+    keys = rng.integers(0, 1 << 20, n, dtype=np.uint64)  # duplicates in every leaf size
+    srt = np.sort(keys)
+    for leaf in (0, 1):
+        k = keys.copy()
+        p = np.arange(n, dtype=np.uint64)
+        arr = (ctypes.c_void_p * 1)(p.ctypes.data)
+        sz = (ctypes.c_uint32 * 1)(8)
+        ns = ctypes.c_double()
+        assert lib.srs_ref_sort_soa_leaf_timed(n, 6, 1, thresh, leaf, k.ctypes.data, 1, arr, sz,
+                                               ctypes.byref(ns)) == 0
+        assert np.array_equal(keys[p.astype(np.int64)], k)  # payloads travel with their keys
+        if leaf == 0 or thresh == 1:
+            assert np.array_equal(k, srt)
+            continue
+        assert np.array_equal(np.sort(k), srt)
+        assert not np.array_equal(k, srt)  # leaves really stay unsorted
+        # each key's slot lies inside its value's sorted run widened by thresh - 1
+        lo = np.searchsorted(srt, k, "left")
+        hi = np.searchsorted(srt, k, "right") - 1
+        i = np.arange(n)
+        assert np.all(i >= lo - (thresh - 1)) and np.all(i <= hi + (thresh - 1))
+
+
 def test_oracle_under_address_and_ub_sanitizers():
     """The C restatement built with -fsanitize=address,undefined (oracle/Makefile
     `asan`) sorts every key kind, both directions, SoA payload

@@ -5,6 +5,11 @@ that GPU numbers sit beside the thesis curves (bachelors-thesis/data/):
                                  n = 1, 2, 4, ... (perf.hpp:366-410)
   <K>[-<P>]-<Dist>-262144.dat    "sort_method nanoseconds_per_element"
                                  (perf.hpp:412-447)
+  cmpThresh-<K>[-<P>]-<Method>-<Dist>.dat  (--thresh) "cmpThresh 262144"
+                                 then "threshold ns_per_element" rows,
+                                 thresholds 2..512 for the insertion-sort
+                                 leaf and 1..262144 for the leaves left
+                                 unsorted (perf.hpp:159-212)
 
 Methods (columns):
   RadixSIMD    the reference itself (oracle/_ref/libsrs_ref.so, AVX-512,
@@ -13,6 +18,10 @@ Methods (columns):
                srs_sort_soa_device; the input is restored between runs)
   GPURadixHost this library through the host-pointer drop-in (srs_sort_soa:
                PCIe both ways included; wall clock)
+  In cmpThresh files the reference's SortMethodRadixSort names
+  (sort_methods.hpp:26-52) are used: RadixSIMD / RadixSIMDNoCmp (the
+  reference with CmpSorterInsertionSort / CmpSorterNoSort) and GPURadix /
+  GPURadixNoCmp (this library, SRS_LEAF_SORTED / SRS_LEAF_UNSORTED).
 
 Repetitions follow perf.hpp:68-69 (max(1, 2^22/n) timed runs after
 max(1, 2^18/n) warm-ups, each on a fresh copy), capped at --max-reps per
@@ -96,27 +105,37 @@ class Methods:
         self.max_reps = max_reps
         self.names = ["RadixSIMD", "GPURadix"] + (["GPURadixHost"] if with_host else [])
 
-    def _ref_once(self, k, p):
+        self.ref.srs_ref_sort_soa_leaf_timed.argtypes = [
+            ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int64, ctypes.c_int,
+            ctypes.c_void_p, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p,
+            ctypes.POINTER(ctypes.c_double)]
+
+    def _ref_once(self, k, p, thresh=16, leaf=0):
         k = k.copy()
         pays = [] if p is None else [p.copy()]
         arr = (ctypes.c_void_p * 1)(*(x.ctypes.data for x in pays)) if pays else None
         sz = (ctypes.c_uint32 * 1)(*(x.itemsize for x in pays)) if pays else None
         ns = ctypes.c_double()
-        rc = self.ref.srs_ref_sort_soa_timed(len(k), self.kind, 1, 16, k.ctypes.data, len(pays),
-                                             arr, sz, ctypes.byref(ns))
+        rc = self.ref.srs_ref_sort_soa_leaf_timed(len(k), self.kind, 1, int(thresh), int(leaf),
+                                                  k.ctypes.data, len(pays), arr, sz,
+                                                  ctypes.byref(ns))
         if rc != 0:
             raise RuntimeError(f"reference sort failed ({rc})")
+        if leaf == 0 and np.any(k[1:] < k[:-1]):  # perf.hpp:118-126 checks the same
+            raise RuntimeError("reference output not sorted")
         return ns.value
 
-    def measure(self, name, k, p):
-        """ns per element, averaged like measureTimePerElementWithRepsAndWarmup."""
+    def measure(self, name, k, p, thresh=16):
+        """ns per element, averaged like measureTimePerElementWithRepsAndWarmup
+        (and measureTimePerElementThreshWithRepsAndWarmup, perf.hpp:131-157)."""
         n = len(k)
         timed, warm = reps(n, self.max_reps)
         torch = self.torch
-        if name == "RadixSIMD":
+        if name in ("RadixSIMD", "RadixSIMDNoCmp"):
+            leaf = 1 if name.endswith("NoCmp") else 0
             for _ in range(warm):
-                self._ref_once(k, p)
-            return sum(self._ref_once(k, p) for _ in range(timed)) / timed / n
+                self._ref_once(k, p, thresh, leaf)
+            return sum(self._ref_once(k, p, thresh, leaf) for _ in range(timed)) / timed / n
         if name == "GPURadixHost":
             def once():
                 kk = k.copy()
@@ -143,12 +162,41 @@ class Methods:
             keys = dk.view(kt[ks])
             pays = [] if dp is None else [dp.view(kt[ps])]
             a.record()
-            self.srs.sort_device(keys, *pays, key_kind=self.kind)
+            self.srs.sort_device(keys, *pays, key_kind=self.kind, cmp_sort_threshold=thresh,
+                                 cmp_sorter="nosort" if name.endswith("NoCmp") else "insertion")
             b.record()
             b.synchronize()
             if r >= warm:
                 tot += a.elapsed_time(b) * 1e6
+        if not name.endswith("NoCmp"):
+            out = dk.view(kt[ks]).cpu().numpy().view(k.dtype)
+            if np.any(out[1:] < out[:-1]):
+                raise RuntimeError(f"{name}: output not sorted")
         return tot / timed / n
+
+
+def thresh_files(m, tname, args, pdt, rng):
+    """perfTestThresh (perf.hpp:159-212): n = 2^18, thresholds doubling from
+    2 to 512 (insertion-sort leaf) or from 1 to n (leaves unsorted), one file
+    per sort method and distribution."""
+    n = 1 << 18
+    dtype = TYPES[tname][0]
+    for dist in args.dists.split(","):
+        k = make(dtype, dist, n, rng)
+        p = None if pdt is None else make(pdt, "Uniform", n, rng)
+        for name in ("RadixSIMD", "RadixSIMDNoCmp", "GPURadix", "GPURadixNoCmp"):
+            lo, hi = (1, n) if name.endswith("NoCmp") else (2, 512)
+            desc = (f"cmpThresh-{tname}" + (f"-{args.payload}" if args.payload else "")
+                    + f"-{name}-{dist}")
+            rows, t = [], lo
+            while t <= hi:
+                rows.append((t, m.measure(name, k, p, thresh=t)))
+                print(desc, t, f"{rows[-1][1]:.3f}", flush=True)
+                t *= 2
+            with open(os.path.join(args.out, desc + ".dat"), "w") as f:
+                f.write(f"cmpThresh {n}\n")
+                for t, v in rows:
+                    f.write(f"{t} {v:.6f}\n")
 
 
 def main():
@@ -160,6 +208,8 @@ def main():
     ap.add_argument("--max-log2", type=int, default=22)
     ap.add_argument("--max-reps", type=int, default=64)
     ap.add_argument("--no-host", action="store_true")
+    ap.add_argument("--thresh", action="store_true",
+                    help="write the cmpThresh-* files (perf.hpp:159-212) instead")
     args = ap.parse_args()
     os.makedirs(args.out, exist_ok=True)
     rng = np.random.default_rng(42)
@@ -167,6 +217,9 @@ def main():
     for tname in args.types.split(","):
         dtype, kind = TYPES[tname]
         m = Methods(kind, pdt, args.max_reps, not args.no_host)
+        if args.thresh:
+            thresh_files(m, tname, args, pdt, rng)
+            continue
         for dist in args.dists.split(","):
             desc = tname + (f"-{args.payload}" if args.payload else "") + f"-{dist}"
             rows = []
