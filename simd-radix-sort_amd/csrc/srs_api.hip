@@ -49,6 +49,16 @@ bool trace_levels() {
   return on;
 }
 
+// SRS_NO_DIRECT_LOCAL=1: the small local class always takes the fast kernel
+// (A/B runs of the direct kernel in one build)
+bool direct_local_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("SRS_NO_DIRECT_LOCAL");
+    return !(e && *e && *e != '0');
+  }();
+  return on;
+}
+
 int fail(int code, const std::string& msg) {
   g_err = msg;
   return code;
@@ -197,7 +207,7 @@ struct Workspace {
   DevBuf tmp2;        // TMP2: AoS records as SoA slice columns (SortDesc::tmp2)
   DevBuf stage;       // device copy of host arrays (host-pointer API)
   DevBuf desc;        // SortDesc
-  DevBuf big[2], local, local2, copy, fallback, fallback2;
+  DevBuf big[2], local, local2, copy, fallback, fallback2, redo;
   DevBuf plan, tcount, gcount, tbase, gbase, var, sbase;
   DevBuf tile_seg, group_seg, hist, offs, gsum, gofs, scan_tmp, totals, ctr;
   DevBuf shist, lut, lut_rbits;  // balanced first level (sampled histogram, digit table)
@@ -896,8 +906,20 @@ int run_sort(Workspace* W, const Request& R, hipStream_t st) {
       const bool rec16 = aos_cols && R.elem_size == 16;
       if (n_local2 > 0)
         launch_local(ksl, d_desc, (Seg*)W->local2.p, n_local2, 1, fb, nfb, st, rec16);
-      if (n_local > 0)
+      // the common SoA shape (4/8-byte key + one 8-byte payload) takes the
+      // direct kernel at four workgroups per CU; what it hands over runs
+      // through the fast kernel
+      const bool direct = !R.aos && R.ncols == 2 && R.widths[1] == 8 && (ks == 4 || ks == 8) &&
+                          !d.canon_zero && !d.tmp2 && direct_local_enabled();
+      if (n_local > 0 && direct) {
+        SRS_TRY(ensure(W->redo, n_local * sizeof(Seg)));
+        launch_local_direct(ks, d_desc, (Seg*)W->local.p, n_local, (Seg*)W->redo.p,
+                            &d_ctr->n_redo, fb1, nfb1, st);
+        launch_local_list(ks, d_desc, (Seg*)W->redo.p, &d_ctr->n_redo,
+                          (int)std::min<int64_t>(n_local, 2048), fb1, nfb1, st);
+      } else if (n_local > 0) {
         launch_local(ksl, d_desc, (Seg*)W->local.p, n_local, 0, fb1, nfb1, st, rec16);
+      }
     }
     {
       TimedScope ts2("local_stable", 0, st);
@@ -923,6 +945,8 @@ int run_sort(Workspace* W, const Request& R, hipStream_t st) {
       fprintf(stderr, "[srs] local: %lld + %lld segs (%llu keys); stable fallback %llu + %llu, "
               "lsd fallback %llu\n", (long long)n_local, (long long)n_local2,
               c.local_elems, c.n_fallback1, c.n_fallback, c.n_fallback2);
+      fprintf(stderr, "[srs] local: %llu small-class segments handed from the direct kernel\n",
+              c.n_redo);
     }
   }
   if (n_copy > 0) {
@@ -1894,7 +1918,7 @@ int srs_release_workspace(void) {
       (void)hipEventSynchronize(w->idle);
       (void)hipEventDestroy(w->idle);
     }
-    DevBuf* bufs[] = {&w->tmp, &w->tmp2, &w->stage, &w->desc, &w->big[0], &w->big[1], &w->local, &w->local2, &w->fallback, &w->fallback2, &w->shist, &w->lut, &w->lut_rbits,
+    DevBuf* bufs[] = {&w->tmp, &w->tmp2, &w->stage, &w->desc, &w->big[0], &w->big[1], &w->local, &w->local2, &w->fallback, &w->fallback2, &w->redo, &w->shist, &w->lut, &w->lut_rbits,
                       &w->copy, &w->plan, &w->tcount, &w->gcount, &w->tbase, &w->gbase,
                       &w->var, &w->sbase, &w->tile_seg, &w->group_seg, &w->hist, &w->offs,
                       &w->gsum, &w->gofs, &w->scan_tmp, &w->totals, &w->ctr,

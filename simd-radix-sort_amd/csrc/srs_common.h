@@ -121,6 +121,7 @@ struct ListCounters {
   unsigned long long n_fallback;  // large-class segments handed to the stable kernel
   unsigned long long n_fallback1; // small-class segments handed to the stable kernel
   unsigned long long n_fallback2; // segments handed on to the LSD local kernel
+  unsigned long long n_redo;      // small-class segments the direct kernel handed to the fast one
 };
 
 // Tuning constants (see DESIGN.md §4 for how they were chosen).
@@ -194,6 +195,20 @@ constexpr int kLocalCapSmall = kLocalThreadsSmall * kLocalItemsSmall;  // 4096
 // occupancy the LDS footprint allows (90 KB -> 1 block/CU; 49 KB -> 3 blocks/CU)
 constexpr int kLocalWavesPerEU = kLocalThreads / 64 / 4;
 constexpr int kLocalWavesPerEUSmall = SRS_LOCAL_SMALL_WGS_PER_CU * kLocalThreadsSmall / 64 / 4;
+// direct local kernel (small class, common SoA shape): 4 workgroups of
+// 256 x 16 per CU
+constexpr int kLocalDirectThreads = 256;
+constexpr int kLocalDirectItems = 4096 / kLocalDirectThreads;
+#ifndef SRS_LOCAL_DIRECT_WGS_PER_CU
+#define SRS_LOCAL_DIRECT_WGS_PER_CU 4
+#endif
+constexpr int kLocalDirectWavesPerEU = SRS_LOCAL_DIRECT_WGS_PER_CU * kLocalDirectThreads / 64 / 4;
+#ifndef SRS_DIRECT_RANK_SPLIT
+#define SRS_DIRECT_RANK_SPLIT 2
+#endif
+#ifndef SRS_DIRECT_EARLY_PAYLOAD
+#define SRS_DIRECT_EARLY_PAYLOAD 0
+#endif
 #ifndef SRS_LOCAL_STABLE_ITEMS
 #define SRS_LOCAL_STABLE_ITEMS 8
 #endif

@@ -2195,6 +2195,233 @@ __global__ __launch_bounds__(NT, WPE) void local_kernel(const SortDesc* __restri
   });
 }
 
+// The fast kernel over a list whose length is known on device only
+// (segments the direct kernel below handed over): grid-stride, so an empty
+// list costs a few microseconds.
+template <typename KT, typename U, int NT, int IT, int WPE>
+__global__ __launch_bounds__(NT, WPE) void local_list_kernel(const SortDesc* __restrict__ desc,
+                                                        const Seg* __restrict__ segs,
+                                                        const unsigned long long* nsegs,
+                                                        Seg* __restrict__ fallback,
+                                                        unsigned long long* fallback_count) {
+  __shared__ FastLds<NT, IT> Ls;
+  const int64_t m = (int64_t)*nsegs;
+  for (int64_t i = blockIdx.x; i < m; i += gridDim.x) {
+    const Seg g = segs[i];
+    local_fast_body<KT, U, NT, IT, false>(desc, g, Ls, [&] {
+      if (threadIdx.x == 0) fallback[atomicAdd(fallback_count, 1ull)] = g;
+    });
+    __syncthreads();  // the next segment reuses the LDS
+  }
+}
+
+// ---- Direct local kernel (round 4): the common SoA shape only -- a dense
+// 4/8-byte key column plus one dense 8-byte payload column, no canon-zero --
+// at four workgroups of 256 x 16 per CU instead of three of 512 x 8.
+// The fast kernel's LDS holds the sort words, a u16 permutation (8 KB) and a
+// bucket-start table (4 KB) beside the packed bucket counters: 49.5 KB, three
+// workgroups per CU. Here the ranked words are written back to their sorted
+// slots (each thread keeps its 16 words and their destinations in registers
+// across one barrier), so no permutation is needed, and the bucket starts are
+// read from the advanced insertion cursors (bucket b's cursor ends at the
+// start of bucket b + 1; cursor word 0 stays 0): 37.4 KB. 16 items per thread
+// at four waves per SIMD leave 128 VGPRs.
+// Everything else (all keys equal, few varying bits (exact), words too wide
+// for (key bits, index)) goes to `redo` for the fast kernel; large buckets
+// go to the stable kernel's list as from the fast kernel.
+template <int NT, int IT>
+struct DirectLds {
+  uint64_t sbuf[NT * IT + kRankSortMax];      // sort words (+ sentinels), then column 1
+  uint32_t cur[(1 << kLocalTopBits) / 2 + 1];  // [0] = 0; bucket b: cur[1 + b/2], half b & 1
+  uint32_t scan_sh[NT / 64 + 1];
+  unsigned long long sh_or;
+  int maxlen;
+};
+
+template <typename KT, typename U, int NT, int IT, int WPE>
+__global__ __launch_bounds__(NT, WPE) void local_direct_kernel(
+    const SortDesc* __restrict__ desc, const Seg* __restrict__ segs, Seg* __restrict__ redo,
+    unsigned long long* redo_count, Seg* __restrict__ fallback,
+    unsigned long long* fallback_count) {
+  constexpr int CAP = NT * IT;
+  constexpr int IDXB = 12;
+  static_assert(CAP <= (1 << IDXB), "index bits");
+  constexpr int NB = 1 << kLocalTopBits;
+  constexpr int BPT = NB / NT;  // bins per thread (an even count: packed pairs)
+  static_assert(BPT * NT == NB && BPT % 2 == 0, "bins per thread");
+  constexpr int KB = (int)sizeof(KT);
+  __shared__ DirectLds<NT, IT> Ls;
+  auto& sbuf = Ls.sbuf;
+  auto& cur = Ls.cur;
+  const Seg g = segs[blockIdx.x];
+  const uint32_t wave = threadIdx.x >> 6;
+  const uint32_t lane = lane_id();
+  const int ebase = (int)wave * IT * 64 + (int)lane;  // element of slot k: ebase + 64 k
+  Xform<U, false> xf;
+  xf.init(*desc);
+  const int cnt = (int)g.len;
+  const int64_t base = g.start;
+  if (threadIdx.x == 0) {
+    Ls.sh_or = 0;
+    Ls.maxlen = 0;
+  }
+  for (uint32_t i = threadIdx.x; i < (uint32_t)(NB / 2 + 1); i += NT) cur[i] = 0;
+
+  // ---- 1. keys ---------------------------------------------------------------
+  uint64_t v0[IT];
+  load_strip<IT, true, KB>(v0, desc->cols[0].base[g.buf], KB, KB, base, ebase, cnt);
+  const U uref = xf((U)ldw<KB>(desc->cols[0].base[g.buf] + base * KB));
+  auto ukey = [&](int k) -> U { return xf((U)v0[k]); };
+  auto valid = [&](int k) -> bool { return ebase + k * 64 < cnt; };
+  U vor = 0;
+#pragma unroll
+  for (int k = 0; k < IT; k++)
+    if (valid(k)) vor |= ukey(k) ^ uref;
+  if (vor) atomicOr(&Ls.sh_or, (unsigned long long)vor);
+  lds_barrier();
+  const unsigned long long var = Ls.sh_or;
+  const int lo = var ? __ffsll((long long)var) - 1 : 0;
+  const int hi = var ? 63 - __clzll((long long)var) : 0;
+  // all keys equal, or few varying bits (the fast kernel's stable exact
+  // pass), or too wide for a (key bits, index) word: the fast kernel
+  if (var == 0 || hi - lo + 1 <= kLocalTopBits || hi + 1 + IDXB > 64) {
+    if (threadIdx.x == 0) redo[atomicAdd(redo_count, 1ull)] = g;
+    return;
+  }
+  const int nbits = kLocalTopBits;
+  const int sh = hi - nbits + 1;
+  const uint32_t mask = (1u << nbits) - 1;
+  const uint64_t keep = (hi == 63) ? ~0ull : ((1ull << (hi + 1)) - 1);
+
+  // ---- 2. bucket histogram (packed 16-bit counters) and insertion cursors ----
+#pragma unroll
+  for (int k = 0; k < IT; k++) {
+    if (valid(k)) {
+      const uint32_t d = (uint32_t)(ukey(k) >> sh) & mask;
+      atomicAdd(&cur[1 + (d >> 1)], 1u << ((d & 1) << 4));
+    }
+  }
+  lds_barrier();
+  {
+    uint32_t tb[BPT], tsum = 0;
+#pragma unroll
+    for (int q = 0; q < BPT; q += 2) {
+      const uint32_t w2 = cur[1 + ((threadIdx.x * BPT + q) >> 1)];
+      tb[q] = w2 & 0xFFFFu;
+      tb[q + 1] = w2 >> 16;
+      tsum += tb[q] + tb[q + 1];
+    }
+    uint32_t ex = block_excl_scan_1b<NT>(tsum, Ls.scan_sh);
+    int mymax = 0;
+#pragma unroll
+    for (int q = 0; q < BPT; q += 2) {
+      const uint32_t e0 = ex, e1 = ex + tb[q];
+      cur[1 + ((threadIdx.x * BPT + q) >> 1)] = e0 | (e1 << 16);
+      ex = e1 + tb[q + 1];
+      mymax = max(mymax, (int)max(tb[q], tb[q + 1]));
+    }
+    if (mymax > 0) atomicMax(&Ls.maxlen, mymax);
+  }
+  lds_barrier();
+  const int maxlen = Ls.maxlen;
+  const bool skip_rank = maxlen <= desc->leaf_skip;  // CmpSorterNoSort leaves (see the fast kernel)
+  if (maxlen > kRankSortMax && !skip_rank) {
+    if (threadIdx.x == 0) fallback[atomicAdd(fallback_count, 1ull)] = g;
+    return;
+  }
+
+  // ---- 3. bucket scatter of the (key bits 0..hi, index) words ----------------
+#pragma unroll
+  for (int k = 0; k < IT; k++) {
+    if (valid(k)) {
+      const U uk = ukey(k);
+      const uint32_t d = (uint32_t)(uk >> sh) & mask;
+      const uint32_t hs = (d & 1) << 4;
+      const uint32_t p = (atomicAdd(&cur[1 + (d >> 1)], 1u << hs) >> hs) & 0xFFFFu;
+      sbuf[p] = (((uint64_t)uk & keep) << IDXB) | (uint64_t)(ebase + k * 64);
+    }
+  }
+  if (threadIdx.x < (uint32_t)kRankSortMax) sbuf[cnt + threadIdx.x] = ~0ull;  // sentinels
+  uint64_t vn[IT];
+#if SRS_DIRECT_EARLY_PAYLOAD
+  load_strip<IT, true, 8>(vn, desc->cols[1].base[g.buf], 8, 8, base, ebase, cnt);
+#endif
+  lds_barrier();
+
+  // ---- 4. rank inside each bucket, then every word to its sorted slot -------
+  if (!skip_rank) {
+    constexpr int NH = SRS_DIRECT_RANK_SPLIT;
+    constexpr int H = IT / NH;
+    uint64_t xs[IT];
+    uint32_t dst[IT];
+#pragma unroll
+    for (int half = 0; half < NH; half++) {
+      uint32_t bs[H], r[H];
+      int wmax = 0;
+#pragma unroll
+      for (int i = 0; i < H; i++) {
+        const int p = (half * H + i) * NT + (int)threadIdx.x;
+        xs[half * H + i] = 0;
+        bs[i] = 0;
+        r[i] = 0;
+        if (p < cnt) {
+          const uint64_t x = sbuf[p];
+          xs[half * H + i] = x;
+          const uint32_t d = (uint32_t)(x >> (sh + IDXB)) & mask;
+          const uint32_t i1 = 1 + (d >> 1);
+          const uint32_t w0 = cur[i1 - 1], w1 = cur[i1];  // (bucket d - 1's end, d's end)
+          const uint32_t s = (d & 1) ? (w1 & 0xFFFFu) : (w0 >> 16);
+          const uint32_t e = (d & 1) ? (w1 >> 16) : (w1 & 0xFFFFu);
+          bs[i] = s;
+          wmax = (int)(e - s) > wmax ? (int)(e - s) : wmax;
+        }
+      }
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) {
+        const int t2 = __shfl_xor(wmax, o, 64);
+        wmax = t2 > wmax ? t2 : wmax;
+      }
+      // (branch-free and unmasked as in the fast kernel: a word past my
+      // bucket's end is a larger key or a ~0 sentinel)
+      for (int j = 0; j < wmax; j++) {
+        uint64_t w[H];
+#pragma unroll
+        for (int i = 0; i < H; i++) w[i] = sbuf[bs[i] + (uint32_t)j];
+#pragma unroll
+        for (int i = 0; i < H; i++) r[i] += w[i] < xs[half * H + i];
+      }
+#pragma unroll
+      for (int i = 0; i < H; i++) dst[half * H + i] = bs[i] + r[i];
+    }
+    lds_barrier();  // every rank read of the bucket-ordered words is done
+#pragma unroll
+    for (int i = 0; i < IT; i++)
+      if (i * NT + (int)threadIdx.x < cnt) sbuf[dst[i]] = xs[i];
+  }
+#if !SRS_DIRECT_EARLY_PAYLOAD
+  load_strip<IT, true, 8>(vn, desc->cols[1].base[g.buf], 8, 8, base, ebase, cnt);
+#endif
+  lds_barrier();
+
+  // ---- 5. column 0 rebuilt from the sorted words, column 1 staged ------------
+  uint32_t id[IT];
+  const uint64_t top = (uint64_t)uref & ~keep;
+  const uint64_t imask = (1u << IDXB) - 1;
+  store_strip<IT, true, KB>(desc->cols[0].base[BUF_OUT], KB, KB, base, ebase, cnt,
+                            [&](int k) -> uint64_t {
+                              const uint64_t w = sbuf[ebase + k * 64];  // < CAP + sentinels
+                              id[k] = (uint32_t)(w & imask);
+                              return (uint64_t)xf.inv((U)(top | (w >> IDXB)));
+                            });
+  lds_barrier();  // every read of the words is done
+#pragma unroll
+  for (int k = 0; k < IT; k++)
+    if (valid(k)) sbuf[ebase + k * 64] = vn[k];
+  lds_barrier();
+  store_strip<IT, true, 8>(desc->cols[1].base[BUF_OUT], 8, 8, base, ebase, cnt,
+                           [&](int k) { return sbuf[id[k]]; });
+}
+
 // Stable path for segments the fast kernel handed over (a top-digit bucket
 // larger than kRankSortMax): the bucket pass ranks with ballots (stable), so
 // buckets whose keys are all equal are final; only mixed buckets are ranked.
@@ -2900,6 +3127,34 @@ void launch_local(int key_size, const SortDesc* d, const Seg* segs, int64_t nseg
 #undef CALL_R
 }
 
+void launch_local_direct(int key_size, const SortDesc* d, const Seg* segs, int64_t nsegs,
+                         Seg* redo, unsigned long long* redo_count, Seg* fallback,
+                         unsigned long long* fallback_count, hipStream_t st) {
+  if (key_size == 4)
+    local_direct_kernel<uint32_t, uint32_t, kLocalDirectThreads, kLocalDirectItems,
+                        kLocalDirectWavesPerEU>
+        <<<(unsigned)nsegs, kLocalDirectThreads, 0, st>>>(d, segs, redo, redo_count, fallback,
+                                                          fallback_count);
+  else
+    local_direct_kernel<uint64_t, uint64_t, kLocalDirectThreads, kLocalDirectItems,
+                        kLocalDirectWavesPerEU>
+        <<<(unsigned)nsegs, kLocalDirectThreads, 0, st>>>(d, segs, redo, redo_count, fallback,
+                                                          fallback_count);
+}
+
+void launch_local_list(int key_size, const SortDesc* d, const Seg* segs,
+                       const unsigned long long* nsegs, int grid, Seg* fallback,
+                       unsigned long long* fallback_count, hipStream_t st) {
+  if (key_size == 4)
+    local_list_kernel<uint32_t, uint32_t, kLocalThreadsSmall, kLocalItemsSmall,
+                      kLocalWavesPerEUSmall>
+        <<<(unsigned)grid, kLocalThreadsSmall, 0, st>>>(d, segs, nsegs, fallback, fallback_count);
+  else
+    local_list_kernel<uint64_t, uint64_t, kLocalThreadsSmall, kLocalItemsSmall,
+                      kLocalWavesPerEUSmall>
+        <<<(unsigned)grid, kLocalThreadsSmall, 0, st>>>(d, segs, nsegs, fallback, fallback_count);
+}
+
 void launch_local_stable(int key_size, const SortDesc* d, const Seg* segs,
                          const unsigned long long* nsegs, int big_class, Seg* fallback,
                          unsigned long long* fallback_count, int grid, hipStream_t st) {
@@ -2986,6 +3241,7 @@ __device__ __forceinline__ void init_lists_body(Seg seg0, int to_local, Seg* big
     ctr->n_fallback = 0;
     ctr->n_fallback1 = 0;
     ctr->n_fallback2 = 0;
+    ctr->n_redo = 0;
     ctr->local_elems = to_local ? (unsigned long long)seg0.len : 0;
     if (to_local) (small ? local : local2)[0] = seg0; else big[0] = seg0;
   }
