@@ -247,6 +247,12 @@ int srs_debug_set_lookback(void* status, void* err);
  * an input exercised a given path. */
 int srs_debug_last_fallbacks(int64_t* counts);
 
+/* Local-level segment counts of the last (non-small) sort on the current
+ * device: counts[0] = segments of the local level, counts[1] = of those, the
+ * ones the direct local kernel handed to the fast kernel.
+ * Synchronizes the device. Tests use it to prove the direct kernel ran. */
+int srs_debug_last_local_counts(int64_t* counts);
+
 /* Release cached device workspaces (for leak checks / shutdown). */
 int srs_release_workspace(void);
 

@@ -906,14 +906,19 @@ int run_sort(Workspace* W, const Request& R, hipStream_t st) {
       const bool rec16 = aos_cols && R.elem_size == 16;
       if (n_local2 > 0)
         launch_local(ksl, d_desc, (Seg*)W->local2.p, n_local2, 1, fb, nfb, st, rec16);
-      // the common SoA shape (4/8-byte key + one 8-byte payload) takes the
-      // direct kernel at four workgroups per CU; what it hands over runs
-      // through the fast kernel
-      const bool direct = !R.aos && R.ncols == 2 && R.widths[1] == 8 && (ks == 4 || ks == 8) &&
-                          !d.canon_zero && !d.tmp2 && direct_local_enabled();
+      // the common shapes take the direct kernel at four workgroups per CU;
+      // what it hands over runs through the fast kernel:
+      // pm 0 a 4/8-byte key + one 8-byte payload (C1), 1 16-byte records of
+      // an 8-byte key as slices (C3), 2 a key + two 4-byte payloads (C2)
+      int pm = -1;
+      if (!R.aos && R.ncols == 2 && R.widths[1] == 8 && !d.tmp2) pm = 0;
+      else if (rec16 && ks == 8) pm = 1;
+      else if (d.pair && ks == 4) pm = 2;
+      const bool direct = pm >= 0 && (ks == 4 || ks == 8) && !d.canon_zero &&
+                          direct_local_enabled();
       if (n_local > 0 && direct) {
         SRS_TRY(ensure(W->redo, n_local * sizeof(Seg)));
-        launch_local_direct(ks, d_desc, (Seg*)W->local.p, n_local, (Seg*)W->redo.p,
+        launch_local_direct(ks, pm, d_desc, (Seg*)W->local.p, n_local, (Seg*)W->redo.p,
                             &d_ctr->n_redo, fb1, nfb1, st);
         launch_local_list(ks, d_desc, (Seg*)W->redo.p, &d_ctr->n_redo,
                           (int)std::min<int64_t>(n_local, 2048), fb1, nfb1, st);
@@ -1874,6 +1879,21 @@ int srs_debug_set_stamp_buffer(void* device_acc) {
 int srs_debug_set_lookback(void* status, void* err) {
   g_lb_status = (uint32_t*)status;
   g_lb_err = (unsigned long long*)err;
+  return SRS_OK;
+}
+
+int srs_debug_last_local_counts(int64_t* counts) {
+  if (!counts) return fail(SRS_ERR_INVALID_ARG, "counts is NULL");
+  Workspace* W = nullptr;
+  std::unique_lock<std::mutex> lk;
+  SRS_TRY(acquire_ws(&W, &lk));
+  counts[0] = counts[1] = 0;
+  if (W->last_small || !W->ctr.p) return SRS_OK;
+  HIP_TRY(hipDeviceSynchronize());
+  ListCounters c;
+  HIP_TRY(hipMemcpy(&c, W->ctr.p, sizeof c, hipMemcpyDeviceToHost));
+  counts[0] = (int64_t)(c.n_local + c.n_local2);
+  counts[1] = (int64_t)c.n_redo;
   return SRS_OK;
 }
 

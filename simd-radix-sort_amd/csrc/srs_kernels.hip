@@ -2215,30 +2215,40 @@ __global__ __launch_bounds__(NT, WPE) void local_list_kernel(const SortDesc* __r
   }
 }
 
-// ---- Direct local kernel (round 4): the common SoA shape only -- a dense
-// 4/8-byte key column plus one dense 8-byte payload column, no canon-zero --
-// at four workgroups of 256 x 16 per CU instead of three of 512 x 8.
+// ---- Direct local kernel (round 3): the common shapes -- a dense 4/8-byte
+// key column with one dense 8-byte payload column (C1), a key with a pair of
+// 4-byte payloads travelling as one word (C2), 16-byte AoS records travelling
+// as two slices (C3); no canon-zero -- at four workgroups of 256 x 16 per CU
+// instead of three of 512 x 8.
 // The fast kernel's LDS holds the sort words, a u16 permutation (8 KB) and a
 // bucket-start table (4 KB) beside the packed bucket counters: 49.5 KB, three
-// workgroups per CU. Here the ranked words are written back to their sorted
-// slots (each thread keeps its 16 words and their destinations in registers
-// across one barrier), so no permutation is needed, and the bucket starts are
-// read from the advanced insertion cursors (bucket b's cursor ends at the
-// start of bucket b + 1; cursor word 0 stays 0): 37.4 KB. 16 items per thread
-// at four waves per SIMD leave 128 VGPRs.
-// Everything else (all keys equal, few varying bits (exact), words too wide
-// for (key bits, index)) goes to `redo` for the fast kernel; large buckets
-// go to the stable kernel's list as from the fast kernel.
+// workgroups per CU. Here every word (key bits lo..hi, index) is written to
+// its sorted slot (each thread keeps its 16 words and their slots in
+// registers across one barrier), so no permutation table is needed, and the
+// key column is rebuilt from the sorted words; the bucket starts are read
+// from the advanced insertion cursors (bucket b's cursor ends at the start
+// of bucket b + 1; cursor word 0 stays 0): 37.4 KB. 16 items per thread at
+// four waves per SIMD leave 128 VGPRs.
+//   exact segments (<= kLocalTopBits varying bits, so a bucket is one key
+//   value): the stable ballot-ranked bucket pass gives every word its slot;
+//   others: the atomic bucket pass, then the rank inside each bucket by word.
+// Handed to the fast kernel (`redo`): all keys equal, more than 52 varying
+// bits, and (PM 1/2) segments outside TMP / TMP2; large buckets of a
+// non-exact segment go to the stable kernel's list as from the fast kernel.
+// PM (payload mode): 0 one dense 8-byte payload column; 1 AoS 16-byte
+// records as two slices in TMP / TMP2, written back as one 16-byte store per
+// record; 2 desc->pair's word column (two 4-byte payloads) in TMP / TMP2,
+// written to the two OUT arrays.
 template <int NT, int IT>
 struct DirectLds {
-  uint64_t sbuf[NT * IT + kRankSortMax];      // sort words (+ sentinels), then column 1
+  uint64_t sbuf[NT * IT + kRankSortMax];      // sort words (+ sentinels), then the payloads
   uint32_t cur[(1 << kLocalTopBits) / 2 + 1];  // [0] = 0; bucket b: cur[1 + b/2], half b & 1
   uint32_t scan_sh[NT / 64 + 1];
   unsigned long long sh_or;
   int maxlen;
 };
 
-template <typename KT, typename U, int NT, int IT, int WPE>
+template <typename KT, typename U, int NT, int IT, int WPE, int PM>
 __global__ __launch_bounds__(NT, WPE) void local_direct_kernel(
     const SortDesc* __restrict__ desc, const Seg* __restrict__ segs, Seg* __restrict__ redo,
     unsigned long long* redo_count, Seg* __restrict__ fallback,
@@ -2247,9 +2257,12 @@ __global__ __launch_bounds__(NT, WPE) void local_direct_kernel(
   constexpr int IDXB = 12;
   static_assert(CAP <= (1 << IDXB), "index bits");
   constexpr int NB = 1 << kLocalTopBits;
+  constexpr int NW = NT / 64;
   constexpr int BPT = NB / NT;  // bins per thread (an even count: packed pairs)
   static_assert(BPT * NT == NB && BPT % 2 == 0, "bins per thread");
+  static_assert(NW * NB * sizeof(uint16_t) <= CAP * sizeof(uint64_t), "per-wave counters");
   constexpr int KB = (int)sizeof(KT);
+  static_assert(PM != 1 || KB == 8, "16-byte records: the key slice is the key");
   __shared__ DirectLds<NT, IT> Ls;
   auto& sbuf = Ls.sbuf;
   auto& cur = Ls.cur;
@@ -2257,10 +2270,17 @@ __global__ __launch_bounds__(NT, WPE) void local_direct_kernel(
   const uint32_t wave = threadIdx.x >> 6;
   const uint32_t lane = lane_id();
   const int ebase = (int)wave * IT * 64 + (int)lane;  // element of slot k: ebase + 64 k
-  Xform<U, false> xf;
-  xf.init(*desc);
   const int cnt = (int)g.len;
   const int64_t base = g.start;
+  auto hand_over = [&](Seg* list, unsigned long long* n) {
+    if (threadIdx.x == 0) list[atomicAdd(n, 1ull)] = g;
+  };
+  if (PM != 0 && g.buf != BUF_TMP && g.buf != BUF_TMP2) {  // (block-uniform)
+    hand_over(redo, redo_count);
+    return;
+  }
+  Xform<U, false> xf;
+  xf.init(*desc);
   if (threadIdx.x == 0) {
     Ls.sh_or = 0;
     Ls.maxlen = 0;
@@ -2279,147 +2299,243 @@ __global__ __launch_bounds__(NT, WPE) void local_direct_kernel(
     if (valid(k)) vor |= ukey(k) ^ uref;
   if (vor) atomicOr(&Ls.sh_or, (unsigned long long)vor);
   lds_barrier();
-  const unsigned long long var = Ls.sh_or;
+  // (LDS values made provably uniform: everything derived from them then
+  // lives in SGPRs, not in the 128 VGPRs)
+  const unsigned long long var_l = Ls.sh_or;
+  const unsigned long long var =
+      ((unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(var_l >> 32))
+       << 32) |
+      (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)var_l);  // (int results: no sign extension)
   const int lo = var ? __ffsll((long long)var) - 1 : 0;
   const int hi = var ? 63 - __clzll((long long)var) : 0;
-  // all keys equal, or few varying bits (the fast kernel's stable exact
-  // pass), or too wide for a (key bits, index) word: the fast kernel
-  if (var == 0 || hi - lo + 1 <= kLocalTopBits || hi + 1 + IDXB > 64) {
-    if (threadIdx.x == 0) redo[atomicAdd(redo_count, 1ull)] = g;
+  const int vbits = hi - lo + 1;
+  // (EX: the exact pass is compiled in; it costs the other modes their
+  // spill-free 128 VGPRs, and only the pair mode (C2's float keys with ~60
+  // copies of each value) meets exact segments in bulk)
+  constexpr bool EX = PM == 2;
+  if (var == 0 || vbits + IDXB > 64 || (!EX && vbits <= kLocalTopBits)) {
+    hand_over(redo, redo_count);
     return;
   }
-  const int nbits = kLocalTopBits;
+  const bool exact = vbits <= kLocalTopBits;
+  const int nbits = exact ? vbits : kLocalTopBits;
   const int sh = hi - nbits + 1;
   const uint32_t mask = (1u << nbits) - 1;
-  const uint64_t keep = (hi == 63) ? ~0ull : ((1ull << (hi + 1)) - 1);
+  const uint64_t vmask = vbits == 64 ? ~0ull : ((1ull << vbits) - 1);
+  // sort word: the varying key bits lo..hi above the element index (the bits
+  // below lo and above hi are uref's)
+  auto word = [&](int k) -> uint64_t {
+    return ((((uint64_t)ukey(k) >> lo) & vmask) << IDXB) | (uint64_t)(ebase + k * 64);
+  };
+  auto digit = [&](int k) -> uint32_t { return (uint32_t)(ukey(k) >> sh) & mask; };
+  // both paths end with word i of this thread (xs) going to its sorted slot
+  // (dst) after one barrier; slot kDump takes the words of empty slots
+  constexpr uint32_t kDump = CAP + kRankSortMax - 1;
+  uint64_t xs[IT];
+  uint32_t dst[IT];
+  bool place = true;
 
-  // ---- 2. bucket histogram (packed 16-bit counters) and insertion cursors ----
+  if (EX && exact) {
+    // ---- 2e. stable bucket pass (ballot ranks, input order inside a bucket):
+    // per-wave counters [NW][nb] in sbuf, bucket starts (u16) in cur; each
+    // word then goes straight to its final slot
+    // (the words are 32-bit here: vbits <= kLocalTopBits, and the digit is
+    // the word's key field; the keys' registers are free from here on)
+    uint16_t* wc = (uint16_t*)sbuf;
+    uint16_t* bstart = (uint16_t*)cur;
+    const uint32_t nb = 1u << nbits;
+    uint32_t w32[IT];
 #pragma unroll
-  for (int k = 0; k < IT; k++) {
-    if (valid(k)) {
-      const uint32_t d = (uint32_t)(ukey(k) >> sh) & mask;
-      atomicAdd(&cur[1 + (d >> 1)], 1u << ((d & 1) << 4));
-    }
-  }
-  lds_barrier();
-  {
-    uint32_t tb[BPT], tsum = 0;
+    for (int k = 0; k < IT; k++) w32[k] = (uint32_t)word(k);
+    auto edigit = [&](int k) -> uint32_t { return w32[k] >> IDXB; };
+    for (uint32_t i = threadIdx.x; i < NW * nb / 2; i += NT) ((uint32_t*)wc)[i] = 0;
+    lds_barrier();
+    uint32_t rank[IT];
+    wlms_rank_fn<IT, kLocalTopBits>(edigit, valid, nbits, &wc[wave * nb], rank);
+    lds_barrier();
+    {
+      uint32_t tb[BPT], tsum = 0;
 #pragma unroll
-    for (int q = 0; q < BPT; q += 2) {
-      const uint32_t w2 = cur[1 + ((threadIdx.x * BPT + q) >> 1)];
-      tb[q] = w2 & 0xFFFFu;
-      tb[q + 1] = w2 >> 16;
-      tsum += tb[q] + tb[q + 1];
-    }
-    uint32_t ex = block_excl_scan_1b<NT>(tsum, Ls.scan_sh);
-    int mymax = 0;
+      for (int q = 0; q < BPT; q++) {
+        const uint32_t b = threadIdx.x * BPT + q;
+        tb[q] = 0;
+        if (b < nb) {
 #pragma unroll
-    for (int q = 0; q < BPT; q += 2) {
-      const uint32_t e0 = ex, e1 = ex + tb[q];
-      cur[1 + ((threadIdx.x * BPT + q) >> 1)] = e0 | (e1 << 16);
-      ex = e1 + tb[q + 1];
-      mymax = max(mymax, (int)max(tb[q], tb[q + 1]));
-    }
-    if (mymax > 0) atomicMax(&Ls.maxlen, mymax);
-  }
-  lds_barrier();
-  const int maxlen = Ls.maxlen;
-  const bool skip_rank = maxlen <= desc->leaf_skip;  // CmpSorterNoSort leaves (see the fast kernel)
-  if (maxlen > kRankSortMax && !skip_rank) {
-    if (threadIdx.x == 0) fallback[atomicAdd(fallback_count, 1ull)] = g;
-    return;
-  }
-
-  // ---- 3. bucket scatter of the (key bits 0..hi, index) words ----------------
-#pragma unroll
-  for (int k = 0; k < IT; k++) {
-    if (valid(k)) {
-      const U uk = ukey(k);
-      const uint32_t d = (uint32_t)(uk >> sh) & mask;
-      const uint32_t hs = (d & 1) << 4;
-      const uint32_t p = (atomicAdd(&cur[1 + (d >> 1)], 1u << hs) >> hs) & 0xFFFFu;
-      sbuf[p] = (((uint64_t)uk & keep) << IDXB) | (uint64_t)(ebase + k * 64);
-    }
-  }
-  if (threadIdx.x < (uint32_t)kRankSortMax) sbuf[cnt + threadIdx.x] = ~0ull;  // sentinels
-  uint64_t vn[IT];
-#if SRS_DIRECT_EARLY_PAYLOAD
-  load_strip<IT, true, 8>(vn, desc->cols[1].base[g.buf], 8, 8, base, ebase, cnt);
-#endif
-  lds_barrier();
-
-  // ---- 4. rank inside each bucket, then every word to its sorted slot -------
-  if (!skip_rank) {
-    constexpr int NH = SRS_DIRECT_RANK_SPLIT;
-    constexpr int H = IT / NH;
-    uint64_t xs[IT];
-    uint32_t dst[IT];
-#pragma unroll
-    for (int half = 0; half < NH; half++) {
-      uint32_t bs[H], r[H];
-      int wmax = 0;
-#pragma unroll
-      for (int i = 0; i < H; i++) {
-        const int p = (half * H + i) * NT + (int)threadIdx.x;
-        xs[half * H + i] = 0;
-        bs[i] = 0;
-        r[i] = 0;
-        if (p < cnt) {
-          const uint64_t x = sbuf[p];
-          xs[half * H + i] = x;
-          const uint32_t d = (uint32_t)(x >> (sh + IDXB)) & mask;
-          const uint32_t i1 = 1 + (d >> 1);
-          const uint32_t w0 = cur[i1 - 1], w1 = cur[i1];  // (bucket d - 1's end, d's end)
-          const uint32_t s = (d & 1) ? (w1 & 0xFFFFu) : (w0 >> 16);
-          const uint32_t e = (d & 1) ? (w1 >> 16) : (w1 & 0xFFFFu);
-          bs[i] = s;
-          wmax = (int)(e - s) > wmax ? (int)(e - s) : wmax;
+          for (int w = 0; w < NW; w++) {
+            const uint32_t c = wc[w * nb + b];
+            wc[w * nb + b] = (uint16_t)tb[q];
+            tb[q] += c;
+          }
         }
+        tsum += tb[q];
       }
+      uint32_t ex = block_excl_scan_1b<NT>(tsum, Ls.scan_sh);
 #pragma unroll
-      for (int o = 32; o >= 1; o >>= 1) {
-        const int t2 = __shfl_xor(wmax, o, 64);
-        wmax = t2 > wmax ? t2 : wmax;
+      for (int q = 0; q < BPT; q++) {
+        const uint32_t b = threadIdx.x * BPT + q;
+        if (b < nb) bstart[b] = (uint16_t)ex;
+        ex += tb[q];
       }
-      // (branch-free and unmasked as in the fast kernel: a word past my
-      // bucket's end is a larger key or a ~0 sentinel)
-      for (int j = 0; j < wmax; j++) {
-        uint64_t w[H];
-#pragma unroll
-        for (int i = 0; i < H; i++) w[i] = sbuf[bs[i] + (uint32_t)j];
-#pragma unroll
-        for (int i = 0; i < H; i++) r[i] += w[i] < xs[half * H + i];
-      }
-#pragma unroll
-      for (int i = 0; i < H; i++) dst[half * H + i] = bs[i] + r[i];
     }
-    lds_barrier();  // every rank read of the bucket-ordered words is done
+    lds_barrier();
 #pragma unroll
-    for (int i = 0; i < IT; i++)
-      if (i * NT + (int)threadIdx.x < cnt) sbuf[dst[i]] = xs[i];
+    for (int k = 0; k < IT; k++) {
+      dst[k] = valid(k) ? rank[k] + bstart[edigit(k)] + wc[wave * nb + edigit(k)] : kDump;
+      xs[k] = w32[k];
+    }
+  } else {
+    // ---- 2. bucket histogram (packed 16-bit counters), insertion cursors ----
+#pragma unroll
+    for (int k = 0; k < IT; k++)
+      if (valid(k)) {
+        const uint32_t d = digit(k);
+        atomicAdd(&cur[1 + (d >> 1)], 1u << ((d & 1) << 4));
+      }
+    lds_barrier();
+    {
+      uint32_t tb[BPT], tsum = 0;
+#pragma unroll
+      for (int q = 0; q < BPT; q += 2) {
+        const uint32_t w2 = cur[1 + ((threadIdx.x * BPT + q) >> 1)];
+        tb[q] = w2 & 0xFFFFu;
+        tb[q + 1] = w2 >> 16;
+        tsum += tb[q] + tb[q + 1];
+      }
+      uint32_t ex = block_excl_scan_1b<NT>(tsum, Ls.scan_sh);
+      int mymax = 0;
+#pragma unroll
+      for (int q = 0; q < BPT; q += 2) {
+        const uint32_t e0 = ex, e1 = ex + tb[q];
+        cur[1 + ((threadIdx.x * BPT + q) >> 1)] = e0 | (e1 << 16);
+        ex = e1 + tb[q + 1];
+        mymax = max(mymax, (int)max(tb[q], tb[q + 1]));
+      }
+      if (mymax > 0) atomicMax(&Ls.maxlen, mymax);
+    }
+    lds_barrier();
+    const int maxlen = __builtin_amdgcn_readfirstlane(Ls.maxlen);
+    // CmpSorterNoSort leaves (see the fast kernel): buckets of <= leaf_skip
+    // keys stay in bucket-pass order
+    const bool skip_rank = maxlen <= desc->leaf_skip;
+    if (maxlen > kRankSortMax && !skip_rank) {  // (block-uniform)
+      hand_over(fallback, fallback_count);
+      return;
+    }
+    // ---- 3. bucket scatter of the words ----------------------------------------
+#pragma unroll
+    for (int k = 0; k < IT; k++) {
+      if (valid(k)) {
+        const uint32_t d = digit(k);
+        const uint32_t hs = (d & 1) << 4;
+        const uint32_t p = (atomicAdd(&cur[1 + (d >> 1)], 1u << hs) >> hs) & 0xFFFFu;
+        sbuf[p] = word(k);
+      }
+    }
+    if (threadIdx.x < (uint32_t)kRankSortMax) sbuf[cnt + threadIdx.x] = ~0ull;  // sentinels
+    lds_barrier();
+    // ---- 4. rank inside each bucket, then every word to its sorted slot ------
+    place = !skip_rank;
+    if (!skip_rank) {
+      constexpr int NH = SRS_DIRECT_RANK_SPLIT;
+      constexpr int H = IT / NH;
+      const int dsh = sh - lo + IDXB;  // the bucket digit's position in a word
+#pragma unroll
+      for (int half = 0; half < NH; half++) {
+        uint32_t bs[H], r[H];
+        int wmax = 0;
+#pragma unroll
+        for (int i = 0; i < H; i++) {
+          const int p = (half * H + i) * NT + (int)threadIdx.x;
+          xs[half * H + i] = 0;
+          bs[i] = 0;
+          r[i] = 0;
+          if (p < cnt) {
+            const uint64_t x = sbuf[p];
+            xs[half * H + i] = x;
+            const uint32_t d = (uint32_t)(x >> dsh) & mask;
+            const uint32_t i1 = 1 + (d >> 1);
+            const uint32_t w0 = cur[i1 - 1], w1 = cur[i1];  // (bucket d - 1's end, d's end)
+            const uint32_t s = (d & 1) ? (w1 & 0xFFFFu) : (w0 >> 16);
+            const uint32_t e = (d & 1) ? (w1 >> 16) : (w1 & 0xFFFFu);
+            bs[i] = s;
+            wmax = (int)(e - s) > wmax ? (int)(e - s) : wmax;
+          }
+        }
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) {
+          const int t2 = __shfl_xor(wmax, o, 64);
+          wmax = t2 > wmax ? t2 : wmax;
+        }
+        // (branch-free and unmasked as in the fast kernel: a word past my
+        // bucket's end is a larger key or a ~0 sentinel)
+        for (int j = 0; j < wmax; j++) {
+          uint64_t w[H];
+#pragma unroll
+          for (int i = 0; i < H; i++) w[i] = sbuf[bs[i] + (uint32_t)j];
+#pragma unroll
+          for (int i = 0; i < H; i++) r[i] += w[i] < xs[half * H + i];
+        }
+#pragma unroll
+        for (int i = 0; i < H; i++)
+          dst[half * H + i] = (half * H + i) * NT + (int)threadIdx.x < cnt ? bs[i] + r[i] : kDump;
+      }
+    }
   }
-#if !SRS_DIRECT_EARLY_PAYLOAD
+  if (place) {  // (block-uniform)
+    lds_barrier();  // every read of the counters / bucket-ordered words is done
+#pragma unroll
+    for (int i = 0; i < IT; i++) sbuf[dst[i]] = xs[i];
+  }
+  // the payloads (dense 8-byte words in every mode)
+  uint64_t vn[IT];
   load_strip<IT, true, 8>(vn, desc->cols[1].base[g.buf], 8, 8, base, ebase, cnt);
-#endif
   lds_barrier();
 
-  // ---- 5. column 0 rebuilt from the sorted words, column 1 staged ------------
+  // ---- 5. keys rebuilt from the sorted words, payloads staged ----------------
   uint32_t id[IT];
-  const uint64_t top = (uint64_t)uref & ~keep;
+  const uint64_t ubase = (uint64_t)uref & ~(vmask << lo);
   const uint64_t imask = (1u << IDXB) - 1;
-  store_strip<IT, true, KB>(desc->cols[0].base[BUF_OUT], KB, KB, base, ebase, cnt,
-                            [&](int k) -> uint64_t {
-                              const uint64_t w = sbuf[ebase + k * 64];  // < CAP + sentinels
-                              id[k] = (uint32_t)(w & imask);
-                              return (uint64_t)xf.inv((U)(top | (w >> IDXB)));
-                            });
+  auto key_of = [&](int k) -> uint64_t {
+    const uint64_t w = sbuf[ebase + k * 64];  // (< CAP + sentinels; past cnt: dropped)
+    id[k] = (uint32_t)(w & imask);
+    return (uint64_t)xf.inv((U)(ubase | ((w >> IDXB) << lo)));
+  };
+  uint64_t ko[IT];
+  if constexpr (PM == 1) {
+#pragma unroll
+    for (int k = 0; k < IT; k++) ko[k] = key_of(k);
+  } else {
+    store_strip<IT, true, KB>(desc->cols[0].base[BUF_OUT], KB, KB, base, ebase, cnt,
+                              [&](int k) { return key_of(k); });
+  }
   lds_barrier();  // every read of the words is done
 #pragma unroll
   for (int k = 0; k < IT; k++)
     if (valid(k)) sbuf[ebase + k * 64] = vn[k];
   lds_barrier();
-  store_strip<IT, true, 8>(desc->cols[1].base[BUF_OUT], 8, 8, base, ebase, cnt,
-                           [&](int k) { return sbuf[id[k]]; });
+  if constexpr (PM == 0) {
+    store_strip<IT, true, 8>(desc->cols[1].base[BUF_OUT], 8, 8, base, ebase, cnt,
+                             [&](int k) { return sbuf[id[k]]; });
+  } else if constexpr (PM == 2) {  // the two halves of each word to their own OUT arrays
+    store_strip<IT, true, 4>(desc->cols[1].base[BUF_OUT], 4, 4, base, ebase, cnt,
+                             [&](int k) { return sbuf[id[k]] & 0xFFFFFFFFull; });
+    store_strip<IT, true, 4>(desc->cols[2].base[BUF_OUT], 4, 4, base, ebase, cnt,
+                             [&](int k) { return sbuf[id[k]] >> 32; });
+  } else {  // {key, payload} records, one 16-byte store each
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    const __amdgpu_buffer_rsrc_t r = strip_rsrc(desc->cols[0].base[BUF_OUT] + base * 16,
+                                                cnt > 0 ? (uint32_t)cnt * 16u : 0u);
+#pragma unroll
+    for (int k = 0; k < IT; k++) {
+      const uint64_t pv = sbuf[id[k]];
+      u32x4 x;
+      x[0] = (uint32_t)ko[k];
+      x[1] = (uint32_t)(ko[k] >> 32);
+      x[2] = (uint32_t)pv;
+      x[3] = (uint32_t)(pv >> 32);
+      __builtin_amdgcn_raw_buffer_store_b128(x, r, (uint32_t)(ebase + k * 64) * 16u, 0, 0);
+    }
+  }
 }
 
 // Stable path for segments the fast kernel handed over (a top-digit bucket
@@ -3127,19 +3243,18 @@ void launch_local(int key_size, const SortDesc* d, const Seg* segs, int64_t nseg
 #undef CALL_R
 }
 
-void launch_local_direct(int key_size, const SortDesc* d, const Seg* segs, int64_t nsegs,
-                         Seg* redo, unsigned long long* redo_count, Seg* fallback,
+void launch_local_direct(int key_size, int pm, const SortDesc* d, const Seg* segs,
+                         int64_t nsegs, Seg* redo, unsigned long long* redo_count, Seg* fallback,
                          unsigned long long* fallback_count, hipStream_t st) {
-  if (key_size == 4)
-    local_direct_kernel<uint32_t, uint32_t, kLocalDirectThreads, kLocalDirectItems,
-                        kLocalDirectWavesPerEU>
-        <<<(unsigned)nsegs, kLocalDirectThreads, 0, st>>>(d, segs, redo, redo_count, fallback,
-                                                          fallback_count);
-  else
-    local_direct_kernel<uint64_t, uint64_t, kLocalDirectThreads, kLocalDirectItems,
-                        kLocalDirectWavesPerEU>
-        <<<(unsigned)nsegs, kLocalDirectThreads, 0, st>>>(d, segs, redo, redo_count, fallback,
-                                                          fallback_count);
+#define CALL(KT, PM)                                                                          \
+  local_direct_kernel<KT, KT, kLocalDirectThreads, kLocalDirectItems, kLocalDirectWavesPerEU, \
+                      PM><<<(unsigned)nsegs, kLocalDirectThreads, 0, st>>>(                   \
+      d, segs, redo, redo_count, fallback, fallback_count)
+  if (pm == 1) CALL(uint64_t, 1);
+  else if (pm == 2) CALL(uint32_t, 2);
+  else if (key_size == 4) CALL(uint32_t, 0);
+  else CALL(uint64_t, 0);
+#undef CALL
 }
 
 void launch_local_list(int key_size, const SortDesc* d, const Seg* segs,

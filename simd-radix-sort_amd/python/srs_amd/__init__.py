@@ -80,6 +80,7 @@ def lib() -> ctypes.CDLL:
     L.srs_partition_device.argtypes = [i64, ctypes.c_int, ctypes.c_int, vp, i32, vp, vp,
                                        ctypes.c_int, vp, i32, vp, vp, vp, vp]
     L.srs_debug_last_fallbacks.argtypes = [ctypes.POINTER(i64)]
+    L.srs_debug_last_local_counts.argtypes = [ctypes.POINTER(i64)]
     L.srs_set_host_devices.argtypes = [i32, vp]
     L.srs_last_error.restype = ctypes.c_char_p
     L.srs_version.restype = ctypes.c_char_p
@@ -370,6 +371,14 @@ def last_fallbacks():
     handed to the stable / LSD fallback kernels (synchronizes the device)."""
     c = (ctypes.c_int64 * 2)()
     _check(lib().srs_debug_last_fallbacks(c))
+    return int(c[0]), int(c[1])
+
+
+def last_local_counts():
+    """(local segments, of which handed from the direct to the fast kernel)
+    of the last sort on the current device (synchronizes the device)."""
+    c = (ctypes.c_int64 * 2)()
+    _check(lib().srs_debug_last_local_counts(c))
     return int(c[0]), int(c[1])
 
 

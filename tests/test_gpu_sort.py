@@ -241,6 +241,89 @@ def test_local_fallback_paths(case, n):
         assert lsd_n == 0, "the stable kernel should have finished these segments"
 
 
+@pytest.mark.parametrize("shape", ["u64+u64", "u32+u64", "i64+u64-down",
+                                   "f32+2xu32", "f32+2xu32-dups", "i32+2xu32-down",
+                                   "rec16-u64", "rec16-f64-down", "u64+u64-exact",
+                                   "u64+u64-wide", "u64+u64-nosort"])
+def test_direct_local_kernel(shape):
+    """The direct local kernel (4 workgroups of 256 x 16 per CU)
+    takes every local segment of the common shapes -- a 4/8-byte key with one
+    8-byte payload (C1), a key with two 4-byte payloads (C2, exact segments
+    included: '-dups' puts ~60 copies on each key value), 16-byte records of
+    an 8-byte key (C3) -- and hands the rest to the fast kernel: segments of
+    <= 11 varying bits in the C1 shape ('-exact'). srs_debug_last_local_counts
+    proves which kernel ran; the result equals a stable sort bit for bit
+    ('-nosort': CmpSorterNoSort leaves, checked against their guarantee).
+    8-byte keys span 50 bits here: at this size one global level leaves up
+    to 55 varying bits of full-range keys, and (key bits, index) words of
+    more than 52 key bits go to the fast kernel's wide mode ('-wide')."""
+    n = (1 << 21) + 77
+    rng = np.random.default_rng(sum(map(ord, shape)))
+    up = not shape.endswith("-down")
+    idx = np.arange(n, dtype=np.uint64)
+    if shape.startswith("rec16"):
+        kind = 9 if "f64" in shape else 6
+        keys = make_keys(kind, "uniform", n, 5)
+        elems = np.empty((n, 16), dtype=np.uint8)
+        elems[:, :8] = keys.view(np.uint8).reshape(n, 8)
+        elems[:, 8:] = idx.view(np.uint8).reshape(n, 8)
+        e = elems.copy()
+        srs_amd.sort_combined(e, kind, up=up)
+        nloc, redo = srs_amd.last_local_counts()
+        assert bytes_equal(e, stable_aos(kind, up, elems))
+        assert nloc > 0 and redo * 100 <= nloc, (nloc, redo)
+        return
+    if "2xu32" in shape:
+        kind = 5 if shape.startswith("i32") else 8
+        if shape.endswith("-dups"):
+            keys = (rng.integers(-(1 << 15), 1 << 15, n) / 32768.0).astype(np.float32)
+        else:
+            keys = make_keys(kind, "uniform", n, 9)
+        p0 = payload_of(keys, 4)
+        p1 = np.arange(n, dtype=np.uint32)
+        k, a, b = keys.copy(), p0.copy(), p1.copy()
+        srs_amd.sort(k, a, b, up=up)
+        nloc, redo = srs_amd.last_local_counts()
+        st = stable_reference(kind, up, [keys, p0, p1])
+        assert bytes_equal(k, st[0]) and bytes_equal(a, st[1]) and bytes_equal(b, st[2])
+        # (a few segments may never have left the input arrays, where the
+        # pair layout does not hold: those go to the fast kernel)
+        assert nloc > 0 and redo * 100 <= nloc, (nloc, redo)
+        return
+    kind = {"u64": 6, "u32": 4, "i64": 7}[shape.split("+")[0]]
+    if shape.endswith("-exact"):  # 2^20 distinct values: ~2 per value, 1-2 bits per segment
+        keys = (rng.integers(0, 1 << 20, n, dtype=np.uint64) << np.uint64(30)).astype(np.uint64)
+    else:
+        keys = make_keys(kind, "uniform", n, 3)
+        if kind != 4 and not shape.endswith("-wide"):
+            keys = keys >> keys.dtype.type(14)
+    k, p = keys.copy(), idx.copy()
+    nosort = shape.endswith("-nosort")
+    if nosort:
+        srs_amd.sort_thresh(16, k, p, cmp_sorter="nosort")
+    else:
+        srs_amd.sort(k, p, up=up)
+    nloc, redo = srs_amd.last_local_counts()
+    assert nloc > 0
+    if shape.endswith("-exact"):
+        assert redo == nloc, (nloc, redo)  # every segment: <= 11 varying bits
+    elif shape.endswith("-wide"):
+        assert 0 < redo < nloc, (nloc, redo)
+    else:
+        assert redo == 0, (nloc, redo)
+    if nosort:
+        assert bytes_equal(keys[p.astype(np.int64)], k)
+        srt = np.sort(keys)
+        lo = np.searchsorted(srt, k, "left")
+        hi = np.searchsorted(srt, k, "right") - 1
+        i = np.arange(n)
+        assert np.all(i >= lo - 15) and np.all(i <= hi + 15)
+        assert not bytes_equal(k, srt)
+        return
+    st = stable_reference(kind, up, [keys, idx])
+    assert bytes_equal(k, st[0]) and bytes_equal(p, st[1])
+
+
 @pytest.mark.parametrize("n", [5000, 50000], ids=["one-launch", "levels"])
 @pytest.mark.parametrize("sizes", [[1], [2], [4], [8], [8, 1], [4, 4], [8, 8, 8], [1] * 63,
                                    [2, 8, 1, 4]])
