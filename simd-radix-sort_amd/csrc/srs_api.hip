@@ -59,6 +59,19 @@ bool direct_local_enabled() {
   return on;
 }
 
+// Fewest small-class segments for which the direct kernel runs. Below it the
+// fast kernel alone is cheaper: the direct kernel's hand-over list costs one
+// more launch (~5-9 us) per sort, and mid-size sorts of 8-byte keys keep more
+// than 52 varying bits per segment after one global level (handed over after
+// one key read). tools/perf_dat.py, u64 + u64 (ns per record, fast only vs
+// with the direct kernel): 2^18 0.373 / 0.427, 2^22 0.068 / 0.079, 2^24
+// 0.0441 / 0.0447; at 1e9 (262144 segments) the direct kernel saves ~0.9 ms.
+// Read on every call (tests lower it to reach the kernel at small sizes).
+int64_t direct_min_segs() {
+  const char* e = getenv("SRS_DIRECT_MIN_SEGS");
+  return (e && *e) ? atoll(e) : 8192;
+}
+
 int fail(int code, const std::string& msg) {
   g_err = msg;
   return code;
@@ -915,7 +928,7 @@ int run_sort(Workspace* W, const Request& R, hipStream_t st) {
       else if (rec16 && ks == 8) pm = 1;
       else if (d.pair && ks == 4) pm = 2;
       const bool direct = pm >= 0 && (ks == 4 || ks == 8) && !d.canon_zero &&
-                          direct_local_enabled();
+                          direct_local_enabled() && n_local >= direct_min_segs();
       if (n_local > 0 && direct) {
         SRS_TRY(ensure(W->redo, n_local * sizeof(Seg)));
         launch_local_direct(ks, pm, d_desc, (Seg*)W->local.p, n_local, (Seg*)W->redo.p,

@@ -257,6 +257,15 @@ def test_direct_local_kernel(shape):
     8-byte keys span 50 bits here: at this size one global level leaves up
     to 55 varying bits of full-range keys, and (key bits, index) words of
     more than 52 key bits go to the fast kernel's wide mode ('-wide')."""
+    import os
+    os.environ["SRS_DIRECT_MIN_SEGS"] = "1"  # (by default only sorts of >= 8192 local segments)
+    try:
+        _direct_local_case(shape)
+    finally:
+        del os.environ["SRS_DIRECT_MIN_SEGS"]
+
+
+def _direct_local_case(shape):
     n = (1 << 21) + 77
     rng = np.random.default_rng(sum(map(ord, shape)))
     up = not shape.endswith("-down")
