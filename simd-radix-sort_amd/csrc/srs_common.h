@@ -203,6 +203,14 @@ constexpr int kLocalDirectItems = 4096 / kLocalDirectThreads;
 #define SRS_LOCAL_DIRECT_WGS_PER_CU 4
 #endif
 constexpr int kLocalDirectWavesPerEU = SRS_LOCAL_DIRECT_WGS_PER_CU * kLocalDirectThreads / 64 / 4;
+// cache-policy bits of the scatter's / the direct local kernel's column
+// loads (buffer-load aux operand; 0 = default)
+#ifndef SRS_SCATTER_LOAD_AUX
+#define SRS_SCATTER_LOAD_AUX 0
+#endif
+#ifndef SRS_LOCAL_LOAD_AUX
+#define SRS_LOCAL_LOAD_AUX 0
+#endif
 #ifndef SRS_DIRECT_RANK_SPLIT
 #define SRS_DIRECT_RANK_SPLIT 2
 #endif

@@ -130,14 +130,15 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t strip_rsrc(const char* base, u
                                            0x00020000);
 }
 
-// voff: per-lane byte offset; soff: wave-uniform byte offset (an SGPR)
-template <int W>
+// voff: per-lane byte offset; soff: wave-uniform byte offset (an SGPR);
+// AUX: the cache-policy bits of the load (0: default)
+template <int W, int AUX = 0>
 __device__ __forceinline__ uint64_t bld(__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff = 0) {
-  if constexpr (W == 1) return __builtin_amdgcn_raw_buffer_load_b8(r, voff, soff, 0);
-  else if constexpr (W == 2) return __builtin_amdgcn_raw_buffer_load_b16(r, voff, soff, 0);
-  else if constexpr (W == 4) return __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0);
+  if constexpr (W == 1) return __builtin_amdgcn_raw_buffer_load_b8(r, voff, soff, AUX);
+  else if constexpr (W == 2) return __builtin_amdgcn_raw_buffer_load_b16(r, voff, soff, AUX);
+  else if constexpr (W == 4) return __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, AUX);
   else {
-    const auto v = __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0);
+    const auto v = __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, AUX);
     return (uint64_t)v[0] | ((uint64_t)v[1] << 32);
   }
 }
@@ -148,7 +149,7 @@ __device__ __forceinline__ uint64_t bld(__amdgpu_buffer_rsrc_t r, uint32_t voff,
 // and a tile's loads stay in flight together (guarded flat loads of 1/2/4-byte
 // columns were each followed by a full vmcnt(0) wait inside loops; C2
 // 29.9 -> 26.0 ms on the same box). Slots past cnt read 0.
-template <int IT, bool DENSE = false, int FW = 0>
+template <int IT, bool DENSE = false, int FW = 0, int AUX = 0>
 __device__ __forceinline__ void load_strip(uint64_t (&dst)[IT], const char* src, uint32_t w,
                                            uint32_t st, int64_t first, int ebase, int cnt) {
   const __amdgpu_buffer_rsrc_t r =
@@ -161,8 +162,8 @@ __device__ __forceinline__ void load_strip(uint64_t (&dst)[IT], const char* src,
     // (a per-slot VGPR offset would be hoisted and held live)
 #pragma unroll
     for (int k = 0; k < IT; k++) {
-      if constexpr (D) dst[k] = bld<W>(r, o0 + (uint32_t)k * 64u * W);
-      else dst[k] = bld<W>(r, o0, __builtin_amdgcn_readfirstlane((uint32_t)k * 64u * st));
+      if constexpr (D) dst[k] = bld<W, AUX>(r, o0 + (uint32_t)k * 64u * W);
+      else dst[k] = bld<W, AUX>(r, o0, __builtin_amdgcn_readfirstlane((uint32_t)k * 64u * st));
     }
   });
 }
@@ -1347,17 +1348,18 @@ __device__ __forceinline__ TileInfo scatter_load_tile(
     ti.cnt = P.skip ? 0 : (rem < kTile ? (int)rem : kTile);
   }
   const int ebase = (int)(threadIdx.x >> 6) * IT * 64 + (int)lane_id();
-  load_strip<IT>(v0, desc->cols[0].base[P.buf], desc->cols[0].width,
-                 desc->cols[0].stride[P.buf], ti.base, ebase, ti.cnt);
+  constexpr int LA = SRS_SCATTER_LOAD_AUX;
+  load_strip<IT, false, 0, LA>(v0, desc->cols[0].base[P.buf], desc->cols[0].width,
+                               desc->cols[0].stride[P.buf], ti.base, ebase, ti.cnt);
   // (desc->pair: in TMP / TMP2 columns 1 and 2 are one 8-byte word column,
   // loaded whole into v1)
   const bool pair_src = PRE3 && desc->pair && (P.buf == BUF_TMP || P.buf == BUF_TMP2);
   if (ncols > 1)
-    load_strip<IT>(v1, desc->cols[1].base[P.buf], pair_src ? 8u : desc->cols[1].width,
-                   desc->cols[1].stride[P.buf], ti.base, ebase, ti.cnt);
+    load_strip<IT, false, 0, LA>(v1, desc->cols[1].base[P.buf], pair_src ? 8u : desc->cols[1].width,
+                                 desc->cols[1].stride[P.buf], ti.base, ebase, ti.cnt);
   if (PRE3 && ncols > 2 && !pair_src)
-    load_strip<IT>(v2, desc->cols[2].base[P.buf], desc->cols[2].width,
-                   desc->cols[2].stride[P.buf], ti.base, ebase, ti.cnt);
+    load_strip<IT, false, 0, LA>(v2, desc->cols[2].base[P.buf], desc->cols[2].width,
+                                 desc->cols[2].stride[P.buf], ti.base, ebase, ti.cnt);
   my_off = 0;
   if (ti.cnt > 0 && threadIdx.x < (1u << P.bits))
     my_off = offs32 ? (int64_t)offs32[t * kMaxBins + threadIdx.x]
@@ -1507,8 +1509,9 @@ __device__ __forceinline__ void scatter_process_tile(
       if (valid(k)) L.sval[pos[k]] = v[k];
     lds_barrier();
     if (c + STEP < ncols)
-      load_strip<IT>(v, desc->cols[c + STEP].base[P.buf], desc->cols[c + STEP].width,
-                     desc->cols[c + STEP].stride[P.buf], ti.base, ebase, cnt);
+      load_strip<IT, false, 0, SRS_SCATTER_LOAD_AUX>(
+          v, desc->cols[c + STEP].base[P.buf], desc->cols[c + STEP].width,
+          desc->cols[c + STEP].stride[P.buf], ti.base, ebase, cnt);
     char* out = desc->cols[c].base[P.dst];
     with_width(cw, [&](auto W_) {
 #pragma unroll
@@ -2290,7 +2293,8 @@ __global__ __launch_bounds__(NT, WPE) void local_direct_kernel(
 
   // ---- 1. keys ---------------------------------------------------------------
   uint64_t v0[IT];
-  load_strip<IT, true, KB>(v0, desc->cols[0].base[g.buf], KB, KB, base, ebase, cnt);
+  load_strip<IT, true, KB, SRS_LOCAL_LOAD_AUX>(v0, desc->cols[0].base[g.buf], KB, KB, base, ebase,
+                                               cnt);
   const U uref = xf((U)ldw<KB>(desc->cols[0].base[g.buf] + base * KB));
   auto ukey = [&](int k) -> U { return xf((U)v0[k]); };
   auto valid = [&](int k) -> bool { return ebase + k * 64 < cnt; };
@@ -2489,7 +2493,8 @@ __global__ __launch_bounds__(NT, WPE) void local_direct_kernel(
   }
   // the payloads (dense 8-byte words in every mode)
   uint64_t vn[IT];
-  load_strip<IT, true, 8>(vn, desc->cols[1].base[g.buf], 8, 8, base, ebase, cnt);
+  load_strip<IT, true, 8, SRS_LOCAL_LOAD_AUX>(vn, desc->cols[1].base[g.buf], 8, 8, base, ebase,
+                                              cnt);
   lds_barrier();
 
   // ---- 5. keys rebuilt from the sorted words, payloads staged ----------------
