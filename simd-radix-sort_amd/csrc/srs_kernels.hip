@@ -2314,6 +2314,23 @@ __global__ __launch_bounds__(NT, WPE) void local_direct_kernel(
   const int lo = var ? __ffsll((long long)var) - 1 : 0;
   const int hi = var ? 63 - __clzll((long long)var) : 0;
   const int vbits = hi - lo + 1;
+#if SRS_DIRECT_WORD_DIGIT
+  // The bucket digit is the top kLocalTopBits bits of the sort word (key bits
+  // lo..hi above the 12-bit element index). With more varying key bits than
+  // that, these are the top varying key bits; with fewer (an "exact"
+  // segment: few distinct values, many copies each) the digit takes the top
+  // index bits too, which spreads each value's copies over buckets by input
+  // position, so buckets stay small and the rank by word (key, index) is the
+  // stable order: no separate exact pass.
+  constexpr bool EX = false;
+  if (var == 0 || vbits + IDXB > 64) {
+    hand_over(redo, redo_count);
+    return;
+  }
+  const bool exact = false;
+  const int nbits = kLocalTopBits;
+  const int dsh = vbits + IDXB - kLocalTopBits;  // the digit's position in a word
+#else
   // (EX: the exact pass is compiled in; it costs the other modes their
   // spill-free 128 VGPRs, and only the pair mode (C2's float keys with ~60
   // copies of each value) meets exact segments in bulk)
@@ -2324,7 +2341,8 @@ __global__ __launch_bounds__(NT, WPE) void local_direct_kernel(
   }
   const bool exact = vbits <= kLocalTopBits;
   const int nbits = exact ? vbits : kLocalTopBits;
-  const int sh = hi - nbits + 1;
+  const int dsh = hi - nbits + 1 - lo + IDXB;  // the digit's position in a word
+#endif
   const uint32_t mask = (1u << nbits) - 1;
   const uint64_t vmask = vbits == 64 ? ~0ull : ((1ull << vbits) - 1);
   // sort word: the varying key bits lo..hi above the element index (the bits
@@ -2332,7 +2350,7 @@ __global__ __launch_bounds__(NT, WPE) void local_direct_kernel(
   auto word = [&](int k) -> uint64_t {
     return ((((uint64_t)ukey(k) >> lo) & vmask) << IDXB) | (uint64_t)(ebase + k * 64);
   };
-  auto digit = [&](int k) -> uint32_t { return (uint32_t)(ukey(k) >> sh) & mask; };
+  auto digit = [&](int k) -> uint32_t { return (uint32_t)(word(k) >> dsh) & mask; };
   // both paths end with word i of this thread (xs) going to its sorted slot
   // (dst) after one barrier; slot kDump takes the words of empty slots
   constexpr uint32_t kDump = CAP + kRankSortMax - 1;
@@ -2443,7 +2461,6 @@ __global__ __launch_bounds__(NT, WPE) void local_direct_kernel(
     if (!skip_rank) {
       constexpr int NH = SRS_DIRECT_RANK_SPLIT;
       constexpr int H = IT / NH;
-      const int dsh = sh - lo + IDXB;  // the bucket digit's position in a word
 #pragma unroll
       for (int half = 0; half < NH; half++) {
         uint32_t bs[H], r[H];

@@ -244,7 +244,7 @@ def test_local_fallback_paths(case, n):
 @pytest.mark.parametrize("shape", ["u64+u64", "u32+u64", "i64+u64-down",
                                    "f32+2xu32", "f32+2xu32-dups", "i32+2xu32-down",
                                    "rec16-u64", "rec16-f64-down", "u64+u64-exact",
-                                   "u64+u64-wide", "u64+u64-nosort"])
+                                   "u64+u64-equal", "u64+u64-wide", "u64+u64-nosort"])
 def test_direct_local_kernel(shape):
     """The direct local kernel (4 workgroups of 256 x 16 per CU)
     takes every local segment of the common shapes -- a 4/8-byte key with one
@@ -256,7 +256,9 @@ def test_direct_local_kernel(shape):
     ('-nosort': CmpSorterNoSort leaves, checked against their guarantee).
     8-byte keys span 50 bits here: at this size one global level leaves up
     to 55 varying bits of full-range keys, and (key bits, index) words of
-    more than 52 key bits go to the fast kernel's wide mode ('-wide')."""
+    more than 52 key bits go to the fast kernel's wide mode ('-wide').
+    Segments of few varying bits ('-exact', '-equal': 3000 copies of each
+    value) go to the fast kernel's exact pass, except in the pair mode."""
     import os
     os.environ["SRS_DIRECT_MIN_SEGS"] = "1"  # (by default only sorts of >= 8192 local segments)
     try:
@@ -303,8 +305,11 @@ def _direct_local_case(shape):
         assert nloc > 0 and redo * 100 <= nloc, (nloc, redo)
         return
     kind = {"u64": 6, "u32": 4, "i64": 7}[shape.split("+")[0]]
-    if shape.endswith("-exact"):  # 2^20 distinct values: ~2 per value, 1-2 bits per segment
+    if shape.endswith("-exact"):  # 2^20 distinct values: ~2 per value, <= 11 bits per segment
         keys = (rng.integers(0, 1 << 20, n, dtype=np.uint64) << np.uint64(30)).astype(np.uint64)
+    elif shape.endswith("-equal"):  # 3000 copies of each value
+        keys = ((np.arange(n, dtype=np.uint64) // np.uint64(3000)) << np.uint64(40))
+        keys = keys[rng.permutation(n)]
     else:
         keys = make_keys(kind, "uniform", n, 3)
         if kind != 4 and not shape.endswith("-wide"):
@@ -317,7 +322,9 @@ def _direct_local_case(shape):
         srs_amd.sort(k, p, up=up)
     nloc, redo = srs_amd.last_local_counts()
     assert nloc > 0
-    if shape.endswith("-exact") or shape.endswith("-wide"):
+    if shape.endswith("-equal") or shape.endswith("-exact"):
+        pass  # (few values per segment, or one: either kernel may take them)
+    elif shape.endswith("-wide"):
         # (the balanced first level's key-range groups need not align with
         # powers of two, so only part of the segments lands in the class)
         assert redo > 0, (nloc, redo)
