@@ -2233,11 +2233,14 @@ __global__ __launch_bounds__(NT, WPE) void local_list_kernel(const SortDesc* __r
 // of bucket b + 1; cursor word 0 stays 0): 37.4 KB. 16 items per thread at
 // four waves per SIMD leave 128 VGPRs.
 //   exact segments (<= kLocalTopBits varying bits, so a bucket is one key
-//   value): the stable ballot-ranked bucket pass gives every word its slot;
+//   value; pair mode only): the stable ballot-ranked bucket pass gives every
+//   word its slot;
 //   others: the atomic bucket pass, then the rank inside each bucket by word.
 // Handed to the fast kernel (`redo`): all keys equal, more than 52 varying
-// bits, and (PM 1/2) segments outside TMP / TMP2; large buckets of a
-// non-exact segment go to the stable kernel's list as from the fast kernel.
+// bits, exact segments outside the pair mode, and (PM 1/2) segments outside
+// TMP / TMP2; large buckets of a non-exact segment go to the stable kernel's
+// list as from the fast kernel. The host runs this kernel only from
+// direct_min_segs() local segments on (srs_api.hip).
 // PM (payload mode): 0 one dense 8-byte payload column; 1 AoS 16-byte
 // records as two slices in TMP / TMP2, written back as one 16-byte store per
 // record; 2 desc->pair's word column (two 4-byte payloads) in TMP / TMP2,
