@@ -253,6 +253,16 @@ int srs_debug_last_fallbacks(int64_t* counts);
  * Synchronizes the device. Tests use it to prove the direct kernel ran. */
 int srs_debug_last_local_counts(int64_t* counts);
 
+/* Placement diagnostics. srs_debug_alloc allocates `bytes` of
+ * device memory on the current device the way mode says (0 = hipMalloc,
+ * 1 = physically contiguous, 2 = hipMemCreate mapped at 1 GiB alignment; the
+ * workspace's own big buffers follow SRS_WS_ALLOC = malloc|contig|vmm);
+ * srs_debug_free releases it. srs_debug_workspace reports the current
+ * device's TMP and TMP2 buffers (NULL / 0 when not allocated). */
+int srs_debug_alloc(uint64_t bytes, int mode, void** ptr);
+int srs_debug_free(void* ptr);
+int srs_debug_workspace(void** tmp, uint64_t* tmp_bytes, void** tmp2, uint64_t* tmp2_bytes);
+
 /* Release cached device workspaces (for leak checks / shutdown). */
 int srs_release_workspace(void);
 

@@ -19,6 +19,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -106,6 +107,7 @@ int key_size_of(int kind) {
 // ---------------------------------------------------------------------------
 struct TimingRec {
   std::string name;
+  std::string name2;  // optional second family (per-level names: "scatter.L1")
   hipEvent_t a, b;
   double elems;
 };
@@ -135,10 +137,11 @@ struct TimedScope {
   bool on = false;
   TimingRec rec;
   hipStream_t st;
-  TimedScope(const char* name, double elems, hipStream_t s) : st(s) {
+  TimedScope(const char* name, double elems, hipStream_t s, int level = 0) : st(s) {
     std::lock_guard<std::mutex> lk(g_tmu);
     if (!g_timing) return;
     rec.name = name;
+    if (level > 0) rec.name2 = std::string(name) + ".L" + std::to_string(level);
     rec.elems = elems;
     rec.a = get_event();
     rec.b = get_event();
@@ -157,9 +160,11 @@ bool timing_enabled() {
   return g_timing;
 }
 
-void note_elems(const char* name, double elems) {
+void note_elems(const char* name, double elems, int level = 0) {
   std::lock_guard<std::mutex> lk(g_tmu);
-  if (g_timing) g_stats[name].elems += elems;
+  if (!g_timing) return;
+  g_stats[name].elems += elems;
+  if (level > 0) g_stats[std::string(name) + ".L" + std::to_string(level)].elems += elems;
 }
 
 void drain_timing_locked() {
@@ -171,6 +176,12 @@ void drain_timing_locked() {
       k.launches++;
       k.ms += ms;
       k.elems += r.elems;
+      if (!r.name2.empty()) {
+        KStat& k2 = g_stats[r.name2];
+        k2.launches++;
+        k2.ms += ms;
+        k2.elems += r.elems;
+      }
     }
     g_event_pool.push_back(r.a);
     g_event_pool.push_back(r.b);
@@ -184,18 +195,109 @@ void drain_timing_locked() {
 struct DevBuf {
   void* p = nullptr;
   size_t bytes = 0;
+  int mode = 0;  // how p was allocated (BigAlloc); 0 = hipMalloc
 };
 
-int ensure(DevBuf& b, size_t bytes) {
+// ---- large-buffer allocation (the O(n) workspace: TMP, TMP2, staging) ------
+// SRS_WS_ALLOC selects how the big workspace buffers are backed (diagnostics
+// of the placement-dependent write rate): "malloc" (default,
+// hipMalloc), "contig" (hipExtMallocWithFlags(hipDeviceMallocContiguous):
+// one physically contiguous range) or "vmm" (hipMemCreate + hipMemMap into a
+// range reserved at 1 GiB alignment).
+enum BigAlloc { ALLOC_MALLOC = 0, ALLOC_CONTIG = 1, ALLOC_VMM = 2 };
+struct VmmRec {
+  hipMemGenericAllocationHandle_t h;
+  size_t size;
+};
+std::mutex g_vmu;
+std::map<void*, VmmRec> g_vmm;
+
+int ws_alloc_mode() {
+  const char* e = getenv("SRS_WS_ALLOC");
+  if (!e || !*e || !strcmp(e, "malloc")) return ALLOC_MALLOC;
+  if (!strcmp(e, "contig")) return ALLOC_CONTIG;
+  if (!strcmp(e, "vmm")) return ALLOC_VMM;
+  return ALLOC_MALLOC;
+}
+
+hipError_t big_alloc(void** p, size_t bytes, int mode) {
+  *p = nullptr;
+  if (mode == ALLOC_CONTIG) return hipExtMallocWithFlags(p, bytes, hipDeviceMallocContiguous);
+  if (mode != ALLOC_VMM) return hipMalloc(p, bytes);
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  hipMemAllocationProp prop = {};
+  prop.type = hipMemAllocationTypePinned;
+  prop.location.type = hipMemLocationTypeDevice;
+  prop.location.id = dev;
+  size_t gran = 0;
+  e = hipMemGetAllocationGranularity(&gran, &prop, hipMemAllocationGranularityRecommended);
+  if (e != hipSuccess) return e;
+  if (gran == 0) gran = size_t(2) << 20;
+  const size_t sz = (bytes + gran - 1) / gran * gran;
+  void* va = nullptr;
+  e = hipMemAddressReserve(&va, sz, size_t(1) << 30, nullptr, 0);
+  if (e != hipSuccess) return e;
+  hipMemGenericAllocationHandle_t h;
+  e = hipMemCreate(&h, sz, &prop, 0);
+  if (e != hipSuccess) {
+    (void)hipMemAddressFree(va, sz);
+    return e;
+  }
+  e = hipMemMap(va, sz, 0, h, 0);
+  if (e == hipSuccess) {
+    hipMemAccessDesc a = {};
+    a.location = prop.location;
+    a.flags = hipMemAccessFlagsProtReadWrite;
+    e = hipMemSetAccess(va, sz, &a, 1);
+    if (e != hipSuccess) (void)hipMemUnmap(va, sz);
+  }
+  if (e != hipSuccess) {
+    (void)hipMemRelease(h);
+    (void)hipMemAddressFree(va, sz);
+    return e;
+  }
+  std::lock_guard<std::mutex> g(g_vmu);
+  g_vmm[va] = VmmRec{h, sz};
+  *p = va;
+  return hipSuccess;
+}
+
+hipError_t big_free(void* p, int mode) {
+  if (!p) return hipSuccess;
+  if (mode != ALLOC_VMM) return hipFree(p);
+  VmmRec r;
+  {
+    std::lock_guard<std::mutex> g(g_vmu);
+    auto it = g_vmm.find(p);
+    if (it == g_vmm.end()) return hipErrorInvalidValue;
+    r = it->second;
+    g_vmm.erase(it);
+  }
+  (void)hipDeviceSynchronize();  // (unmapping does not wait for queued kernels)
+  hipError_t e = hipMemUnmap(p, r.size);
+  hipError_t e2 = hipMemRelease(r.h);
+  hipError_t e3 = hipMemAddressFree(p, r.size);
+  return e != hipSuccess ? e : e2 != hipSuccess ? e2 : e3;
+}
+
+void free_buf(DevBuf& b) {
+  if (b.p) (void)big_free(b.p, b.mode);
+  b = DevBuf();
+}
+
+int ensure(DevBuf& b, size_t bytes, int mode = ALLOC_MALLOC) {
   if (b.bytes >= bytes && b.p) return SRS_OK;
   if (b.p) {
-    HIP_TRY(hipFree(b.p));
+    HIP_TRY(big_free(b.p, b.mode));
     b.p = nullptr;
     b.bytes = 0;
   }
   size_t want = std::max<size_t>(bytes, 256);
-  HIP_TRY(hipMalloc(&b.p, want));
+  HIP_TRY(big_alloc(&b.p, want, mode));
   b.bytes = want;
+  b.mode = mode;
   return SRS_OK;
 }
 
@@ -246,12 +348,38 @@ struct Workspace {
   // one call at a time per device (calls on different devices run in
   // parallel: the multi-GPU host split sorts its shards from several threads)
   std::mutex mu;
+  // Freed when the last holder lets go (srs_release_workspace only drops the
+  // registry's reference, so a call that has looked the workspace up keeps
+  // it alive until it returns).
+  ~Workspace() {
+    if (idle) {  // the last call's kernels may still read the buffers
+      (void)hipEventSynchronize(idle);
+      (void)hipEventDestroy(idle);
+    }
+    DevBuf* bufs[] = {&tmp, &tmp2, &stage, &desc, &big[0], &big[1], &local, &local2, &fallback,
+                      &fallback2, &redo, &shist, &lut, &lut_rbits, &copy, &plan, &tcount,
+                      &gcount, &tbase, &gbase, &var, &sbase, &tile_seg, &group_seg, &hist, &offs,
+                      &gsum, &gofs, &scan_tmp, &totals, &ctr, &prun, &ptile, &btot, &bnt, &btile,
+                      &nt_over, &gtile, &gorder};
+    for (DevBuf* b : bufs) free_buf(*b);
+    for (auto& t : small_taken) free_buf(t.second);
+    if (h_ctr) (void)hipHostFree(h_ctr);
+    if (h_totals) (void)hipHostFree(h_totals);
+    (void)hipGetLastError();  // (release-time failures leave no sticky error behind)
+  }
 };
 
 std::mutex g_wmu;  // the map below
-std::map<int, Workspace*> g_ws;
+std::map<int, std::shared_ptr<Workspace>> g_ws;
 
-int get_ws_locked(Workspace** out) {
+// A workspace held for one call: the reference keeps it alive, the lock
+// (taken after the lookup, released first) makes the call its only user.
+struct WsLock {
+  std::shared_ptr<Workspace> ref;
+  std::unique_lock<std::mutex> lk;
+};
+
+int get_ws_locked(std::shared_ptr<Workspace>* out) {
   int dev = 0;
   HIP_TRY(hipGetDevice(&dev));
   auto it = g_ws.find(dev);
@@ -259,7 +387,7 @@ int get_ws_locked(Workspace** out) {
     *out = it->second;
     return SRS_OK;
   }
-  Workspace* w = new Workspace();
+  auto w = std::make_shared<Workspace>();
   HIP_TRY(hipHostMalloc((void**)&w->h_ctr, sizeof(ListCounters), hipHostMallocDefault));
   HIP_TRY(hipHostMalloc((void**)&w->h_totals, 4 * sizeof(uint64_t), hipHostMallocDefault));
   g_ws[dev] = w;
@@ -267,13 +395,17 @@ int get_ws_locked(Workspace** out) {
   return SRS_OK;
 }
 
-// The current device's workspace, locked for this call (lk holds W->mu).
-int acquire_ws(Workspace** out, std::unique_lock<std::mutex>* lk) {
+// The current device's workspace, locked for this call (lk holds a reference
+// and W->mu).
+int acquire_ws(Workspace** out, WsLock* lk) {
+  std::shared_ptr<Workspace> w;
   {
     std::lock_guard<std::mutex> g(g_wmu);
-    SRS_TRY(get_ws_locked(out));
+    SRS_TRY(get_ws_locked(&w));
   }
-  *lk = std::unique_lock<std::mutex>((*out)->mu);
+  lk->lk = std::unique_lock<std::mutex>(w->mu);
+  lk->ref = std::move(w);
+  *out = lk->ref.get();
   return SRS_OK;
 }
 
@@ -466,6 +598,7 @@ struct LevelState {
   int ncols;               // columns moved with the keys (SortDesc::ncols)
   int tmp2;                // SortDesc::tmp2
   int64_t known_len = -1;  // the length of the single big segment, when the host knows it
+  int level = 0;           // global levels run so far (per-level timing names)
 };
 
 // One global MSB level over every large segment in W->big[S.cur]:
@@ -535,9 +668,10 @@ int run_level(Workspace* W, int ks, const SortDesc* d_desc, LevelState& S, int f
     level_keys = W->h_totals[3];
   }
   S.known_len = -1;
+  const int lv = ++S.level;
   const double level_elems = (double)level_keys;
-  note_elems("count", level_elems);
-  note_elems("scatter", level_elems);
+  note_elems("count", level_elems, lv);
+  note_elems("scatter", level_elems, lv);
 
   SRS_TRY(ensure(W->tile_seg, ntiles * 4));
   SRS_TRY(ensure(W->group_seg, ngroups * 4));
@@ -553,7 +687,7 @@ int run_level(Workspace* W, int ks, const SortDesc* d_desc, LevelState& S, int f
   launch_seg_map2((int64_t*)W->tbase.p, ntiles, tile_seg, (int64_t*)W->gbase.p, ngroups,
                   group_seg, nbig, st);
   {
-    TimedScope ts("count", (double)0, st);
+    TimedScope ts("count", (double)0, st, lv);
     launch_count(ks, d_desc, plan, tile_seg, ntiles, (uint16_t*)W->hist.p, var, lut, st, M.gt,
                  M.torder);
   }
@@ -578,7 +712,7 @@ int run_level(Workspace* W, int ks, const SortDesc* d_desc, LevelState& S, int f
   if (g_lb_status)  // (diagnostic look-back: fresh status words per level)
     HIP_TRY(hipMemsetAsync(g_lb_status, 0, (size_t)ntiles * kMaxBins * 4, st));
   {
-    TimedScope ts("scatter", (double)0, st);
+    TimedScope ts("scatter", (double)0, st, lv);
     launch_scatter(ks, d_desc, plan, tile_seg, (uint64_t*)W->offs.p,
                    offs32 ? (const uint32_t*)W->offs.p : nullptr, ntiles, lut, S.ncols, st,
                    M.gt);
@@ -693,6 +827,46 @@ int run_small(Workspace* W, const Request& R, hipStream_t st) {
   return SRS_OK;
 }
 
+// The column layout local_direct_kernel's mode pm writes without checking
+// (it stores whole records / dense words): pm 0 a dense key column and one
+// dense 8-byte payload column; pm 1 16-byte records of an 8-byte key, the two
+// slices at +0 / +8 of each record in IN / OUT and dense 8-byte slice columns
+// in TMP / TMP2; pm 2 a dense key column and the two 4-byte payloads as one
+// interleaved 8-byte word column in TMP / TMP2 (SortDesc::pair).
+bool direct_layout_ok(const SortDesc& d, int pm, int ks) {
+  const Col& k = d.cols[0];
+  const int bufs[] = {BUF_IN, BUF_OUT, BUF_TMP, BUF_TMP2};
+  if (pm == 0) {
+    if (d.ncols != 2 || d.tmp2 || d.cols[1].width != 8 || k.width != (uint32_t)ks) return false;
+    for (int b : {BUF_IN, BUF_OUT, BUF_TMP})
+      if (k.stride[b] != k.width || d.cols[1].stride[b] != 8) return false;
+    return true;
+  }
+  if (pm == 1) {
+    const Col& p = d.cols[1];
+    if (d.ncols != 2 || !d.tmp2 || ks != 8 || k.width != 8 || p.width != 8) return false;
+    for (int b : {BUF_IN, BUF_OUT})
+      if (k.stride[b] != 16 || p.stride[b] != 16 || p.base[b] != k.base[b] + 8) return false;
+    for (int b : {BUF_TMP, BUF_TMP2})
+      if (k.stride[b] != 8 || p.stride[b] != 8) return false;
+    return true;
+  }
+  if (pm == 2) {
+    const Col& a = d.cols[1];
+    const Col& c = d.cols[2];
+    if (d.ncols != 3 || !d.pair || a.width != 4 || c.width != 4 || k.width != (uint32_t)ks)
+      return false;
+    for (int b : bufs)
+      if (k.stride[b] != k.width) return false;
+    for (int b : {BUF_IN, BUF_OUT})
+      if (a.stride[b] != 4 || c.stride[b] != 4) return false;
+    for (int b : {BUF_TMP, BUF_TMP2})
+      if (a.stride[b] != 8 || c.stride[b] != 8 || c.base[b] != a.base[b] + 4) return false;
+    return true;
+  }
+  return false;
+}
+
 constexpr int64_t kStripeMinN = int64_t(1) << 25;
 
 bool stripes_enabled() {
@@ -705,6 +879,10 @@ bool stripes_enabled() {
 
 int run_sort(Workspace* W, const Request& R, hipStream_t st) {
   if (R.nsegs == 0 && R.num <= kLocalCap) return run_small(W, R, st);
+  {
+    const char* e = getenv("SRS_XCD_ROT");  // (placement diagnostics)
+    set_xcd_rotation(e && *e ? atoi(e) : 0);
+  }
   W->last_small = false;
   const int ks = key_size_of(R.kind);
   const int64_t n = R.num;
@@ -743,11 +921,11 @@ int run_sort(Workspace* W, const Request& R, hipStream_t st) {
       tmp_bytes += align_up((size_t)n * R.widths[c], 256);  // (a pair: 8n bytes at tmp_off[1])
     }
   }
-  SRS_TRY(ensure(W->tmp, tmp_bytes));
+  SRS_TRY(ensure(W->tmp, tmp_bytes, ws_alloc_mode()));
   char* tmp = (char*)W->tmp.p;
   char* tmp2 = nullptr;
   if (aos_cols || pair_cols) {
-    SRS_TRY(ensure(W->tmp2, tmp_bytes));
+    SRS_TRY(ensure(W->tmp2, tmp_bytes, ws_alloc_mode()));
     tmp2 = (char*)W->tmp2.p;
     d.tmp2 = 1;
   }
@@ -927,6 +1105,7 @@ int run_sort(Workspace* W, const Request& R, hipStream_t st) {
       if (!R.aos && R.ncols == 2 && R.widths[1] == 8 && !d.tmp2) pm = 0;
       else if (rec16 && ks == 8) pm = 1;
       else if (d.pair && ks == 4) pm = 2;
+      if (pm >= 0 && !direct_layout_ok(d, pm, ks)) pm = -1;  // (the kernel assumes it)
       const bool direct = pm >= 0 && (ks == 4 || ks == 8) && !d.canon_zero &&
                           direct_local_enabled() && n_local >= direct_min_segs();
       if (n_local > 0 && direct) {
@@ -1077,7 +1256,7 @@ bool whole_input_is_unsorted_leaf(const Request& R) {
 int sort_device(Request& R, hipStream_t st) {
   if (R.num <= 1 || whole_input_is_unsorted_leaf(R)) return copy_through(R, st);
   Workspace* W = nullptr;
-  std::unique_lock<std::mutex> lk;
+  WsLock lk;
   SRS_TRY(acquire_ws(&W, &lk));
   // (a small sort touches no workspace buffer but its stream's debug slot)
   if (R.num <= kLocalCap) return run_small(W, R, st);
@@ -1115,19 +1294,38 @@ struct HostStage {  // per device, kept between calls
   hipStream_t cst[kStageThreads] = {};  // copy streams (one per host thread)
   hipEvent_t ev[kStageThreads][kStageBufs] = {};
   hipStream_t st = nullptr;             // the sort's stream
+  // freed when the last holder lets go (as Workspace)
+  ~HostStage() {
+    for (int t = 0; t < kStageThreads; t++) {
+      if (cst[t]) (void)hipStreamSynchronize(cst[t]);
+      for (int b = 0; b < kStageBufs; b++) {
+        if (pin[t][b]) (void)hipHostFree(pin[t][b]);
+        if (ev[t][b]) (void)hipEventDestroy(ev[t][b]);
+      }
+      if (cst[t]) (void)hipStreamDestroy(cst[t]);
+    }
+    if (st) {
+      (void)hipStreamSynchronize(st);
+      (void)hipStreamDestroy(st);
+    }
+    (void)hipGetLastError();  // (nothing above may leave a sticky error behind)
+  }
 };
+using StageRef = std::shared_ptr<HostStage>;
 std::mutex g_smu;
-std::map<int, HostStage*> g_stage;
+std::map<int, StageRef> g_stage;
 
-// (the calling thread's current device is `dev`)
-int get_stage(int dev, HostStage** out) {
+// (the calling thread's current device is `dev`). The caller holds the
+// returned reference for as long as it uses the stage, so
+// srs_release_workspace can never free a stage under a running sort.
+int get_stage(int dev, StageRef* out) {
   std::lock_guard<std::mutex> g(g_smu);
   auto it = g_stage.find(dev);
   if (it != g_stage.end()) {
     *out = it->second;
     return SRS_OK;
   }
-  HostStage* S = new HostStage();
+  auto S = std::make_shared<HostStage>();
   S->dev = dev;
   for (int t = 0; t < kStageThreads; t++) {
     HIP_TRY(hipStreamCreateWithFlags(&S->cst[t], hipStreamNonBlocking));
@@ -1142,27 +1340,14 @@ int get_stage(int dev, HostStage** out) {
   return SRS_OK;
 }
 
+// Drops the registry's references; each stage is freed by its last holder.
 void release_host_stages() {
-  std::lock_guard<std::mutex> g(g_smu);
-  for (auto& kv : g_stage) {
-    HostStage* S = kv.second;
-    { std::lock_guard<std::mutex> busy(S->mu); }  // no call is using it any more
-    for (int t = 0; t < kStageThreads; t++) {
-      if (S->cst[t]) (void)hipStreamSynchronize(S->cst[t]);
-      for (int b = 0; b < kStageBufs; b++) {
-        if (S->pin[t][b]) (void)hipHostFree(S->pin[t][b]);
-        if (S->ev[t][b]) (void)hipEventDestroy(S->ev[t][b]);
-      }
-      if (S->cst[t]) (void)hipStreamDestroy(S->cst[t]);
-    }
-    if (S->st) {
-      (void)hipStreamSynchronize(S->st);
-      (void)hipStreamDestroy(S->st);
-    }
-    delete S;  // (after its lock is released: the lock lives inside S)
+  std::map<int, StageRef> old;
+  {
+    std::lock_guard<std::mutex> g(g_smu);
+    old.swap(g_stage);
   }
-  g_stage.clear();
-  (void)hipGetLastError();  // (nothing above may leave a sticky error behind)
+  old.clear();  // (outside g_smu: a destructor waits for the stage's streams)
 }
 
 // One thread's stripe [a, a + len) of a host <-> device copy through its ring.
@@ -1249,11 +1434,12 @@ size_t col_width(const Request& R, int c) { return R.aos ? R.elem_size : R.width
 int host_sort_single(Request& R, int dev) {
   DeviceGuard keep;
   HIP_TRY(hipSetDevice(dev));
-  HostStage* S = nullptr;
-  SRS_TRY(get_stage(dev, &S));
+  StageRef Sref;
+  SRS_TRY(get_stage(dev, &Sref));
+  HostStage* S = Sref.get();
   std::lock_guard<std::mutex> slk(S->mu);
   Workspace* W = nullptr;
-  std::unique_lock<std::mutex> lk;
+  WsLock lk;
   SRS_TRY(acquire_ws(&W, &lk));
   std::vector<size_t> off;
   size_t total = 0;
@@ -1325,19 +1511,24 @@ struct ShardBufs {  // device buffers of one shard, kept between calls
   int dev = 0;
   DevBuf in, part, recv, hist, lut;
 };
-std::mutex g_shmu;
-std::vector<ShardBufs*> g_shards;
+// One split at a time: the shard buffers are shared by every split call,
+// and a call uses them across all of its phases (also from its per-shard
+// threads). Held for the whole of host_sort_split and by
+// srs_release_workspace around freeing them. Lock order: g_split_mu, then
+// g_smu / HostStage::mu, then g_wmu / Workspace::mu.
+std::mutex g_split_mu;
+std::vector<ShardBufs*> g_shards;  // (under g_split_mu)
 
-ShardBufs* shard_bufs(int g, int dev) {
-  std::lock_guard<std::mutex> lk(g_shmu);
+void free_shard(ShardBufs* B) {
+  DevBuf* bufs[] = {&B->in, &B->part, &B->recv, &B->hist, &B->lut};
+  for (DevBuf* b : bufs) free_buf(*b);
+}
+
+ShardBufs* shard_bufs(int g, int dev) {  // (g_split_mu held)
   while ((int)g_shards.size() <= g) g_shards.push_back(new ShardBufs());
   ShardBufs* B = g_shards[g];
   if (B->dev != dev) {  // (another device list than last time)
-    DevBuf* bufs[] = {&B->in, &B->part, &B->recv, &B->hist, &B->lut};
-    for (DevBuf* b : bufs) {
-      if (b->p) (void)hipFree(b->p);
-      *b = DevBuf();
-    }
+    free_shard(B);
     B->dev = dev;
   }
   return B;
@@ -1361,6 +1552,7 @@ int for_shards(int G, F f) {
 }
 
 int host_sort_split(Request& R, const std::vector<int>& devs) {
+  std::lock_guard<std::mutex> split(g_split_mu);
   const int G = (int)devs.size();
   const int64_t n = R.num;
   const int ks = key_size_of(R.kind);
@@ -1374,7 +1566,7 @@ int host_sort_split(Request& R, const std::vector<int>& devs) {
   int64_t maxchunk = 0;
   for (int g = 0; g < G; g++) maxchunk = std::max(maxchunk, lo[g + 1] - lo[g]);
   std::vector<ShardBufs*> B(G);
-  std::vector<HostStage*> S(G);
+  std::vector<StageRef> S(G);
   for (int g = 0; g < G; g++) B[g] = shard_bufs(g, devs[g]);
   std::vector<std::vector<uint64_t>> hist(G, std::vector<uint64_t>(nbins));
 
@@ -1394,7 +1586,7 @@ int host_sort_split(Request& R, const std::vector<int>& devs) {
     SRS_TRY(ensure(B[g]->hist, nbins * sizeof(uint64_t)));
     const int64_t m = lo[g + 1] - lo[g];
     for (int c = 0; c < R.ncols; c++)
-      SRS_TRY(staged_copy(S[g], (char*)B[g]->in.p + off[c],
+      SRS_TRY(staged_copy(S[g].get(), (char*)B[g]->in.p + off[c],
                           (char*)R.in_cols[c] + (size_t)lo[g] * R.widths[c],
                           (size_t)m * R.widths[c], true));
     hipStream_t st = S[g]->st;
@@ -1460,7 +1652,7 @@ int host_sort_split(Request& R, const std::vector<int>& devs) {
       return SRS_OK;
     }
     Workspace* W = nullptr;
-    std::unique_lock<std::mutex> lk;
+    WsLock lk;
     SRS_TRY(acquire_ws(&W, &lk));
     WsUse use;
     SRS_TRY(use.begin(W, st));
@@ -1521,7 +1713,7 @@ int host_sort_split(Request& R, const std::vector<int>& devs) {
     }
     {
       Workspace* W = nullptr;
-      std::unique_lock<std::mutex> lk;
+      WsLock lk;
       SRS_TRY(acquire_ws(&W, &lk));
       if (m > 1 && !whole_input_is_unsorted_leaf(D)) {
         if (m <= kLocalCap) {
@@ -1535,7 +1727,7 @@ int host_sort_split(Request& R, const std::vector<int>& devs) {
       HIP_TRY(hipStreamSynchronize(st));
     }
     for (int c = 0; c < R.ncols; c++)
-      SRS_TRY(staged_copy(S[h], (char*)D.out_cols[c],
+      SRS_TRY(staged_copy(S[h].get(), (char*)D.out_cols[c],
                           (char*)R.out_cols[c] + (size_t)rstart[h] * R.widths[c],
                           (size_t)m * R.widths[c], false));
     return SRS_OK;
@@ -1733,7 +1925,7 @@ int srs_sort_segments_device(int64_t num, int key_kind, int up, void* keys,
   R.nsegs = num_segments;
   R.known_top_bits = known_top_bits;
   Workspace* W = nullptr;
-  std::unique_lock<std::mutex> lk;
+  WsLock lk;
   SRS_TRY(acquire_ws(&W, &lk));
   WsUse use;
   SRS_TRY(use.begin(W, (hipStream_t)stream));
@@ -1831,7 +2023,7 @@ int srs_partition_device(int64_t num, int key_kind, int up, const void* keys,
     return copy_through(R, (hipStream_t)stream);
   }
   Workspace* W = nullptr;
-  std::unique_lock<std::mutex> lk;
+  WsLock lk;
   SRS_TRY(acquire_ws(&W, &lk));
   WsUse use;
   SRS_TRY(use.begin(W, (hipStream_t)stream));
@@ -1840,7 +2032,10 @@ int srs_partition_device(int64_t num, int key_kind, int up, const void* keys,
 
 const char* srs_last_error(void) { return g_err.c_str(); }
 
-const char* srs_version(void) { return "srs_amd 0.1.0 gfx950"; }
+#ifndef SRS_SRC_HASH
+#define SRS_SRC_HASH "unknown"
+#endif
+const char* srs_version(void) { return "srs_amd 0.1.0 gfx950 src:" SRS_SRC_HASH; }
 
 int srs_set_host_devices(int32_t num_devices, const int32_t* devices) {
   if (num_devices < 0 || num_devices > 512 || (num_devices > 0 && !devices))
@@ -1898,7 +2093,7 @@ int srs_debug_set_lookback(void* status, void* err) {
 int srs_debug_last_local_counts(int64_t* counts) {
   if (!counts) return fail(SRS_ERR_INVALID_ARG, "counts is NULL");
   Workspace* W = nullptr;
-  std::unique_lock<std::mutex> lk;
+  WsLock lk;
   SRS_TRY(acquire_ws(&W, &lk));
   counts[0] = counts[1] = 0;
   if (W->last_small || !W->ctr.p) return SRS_OK;
@@ -1913,7 +2108,7 @@ int srs_debug_last_local_counts(int64_t* counts) {
 int srs_debug_last_fallbacks(int64_t* counts) {
   if (!counts) return fail(SRS_ERR_INVALID_ARG, "counts is NULL");
   Workspace* W = nullptr;
-  std::unique_lock<std::mutex> lk;
+  WsLock lk;
   SRS_TRY(acquire_ws(&W, &lk));
   counts[0] = counts[1] = 0;
   if (W->last_small) {
@@ -1931,41 +2126,58 @@ int srs_debug_last_fallbacks(int64_t* counts) {
   return SRS_OK;
 }
 
+std::mutex g_dbg_amu;
+std::map<void*, int> g_dbg_allocs;  // srs_debug_alloc: pointer -> mode
+
+int srs_debug_alloc(uint64_t bytes, int mode, void** ptr) {
+  if (!ptr || mode < ALLOC_MALLOC || mode > ALLOC_VMM || bytes == 0)
+    return fail(SRS_ERR_INVALID_ARG, "srs_debug_alloc: ptr, mode 0..2 and bytes > 0");
+  HIP_TRY(big_alloc(ptr, (size_t)bytes, mode));
+  std::lock_guard<std::mutex> g(g_dbg_amu);
+  g_dbg_allocs[*ptr] = mode;
+  return SRS_OK;
+}
+
+int srs_debug_free(void* ptr) {
+  int mode = 0;
+  {
+    std::lock_guard<std::mutex> g(g_dbg_amu);
+    auto it = g_dbg_allocs.find(ptr);
+    if (it == g_dbg_allocs.end()) return fail(SRS_ERR_INVALID_ARG, "srs_debug_free: unknown pointer");
+    mode = it->second;
+    g_dbg_allocs.erase(it);
+  }
+  HIP_TRY(big_free(ptr, mode));
+  return SRS_OK;
+}
+
+int srs_debug_workspace(void** tmp, uint64_t* tmp_bytes, void** tmp2, uint64_t* tmp2_bytes) {
+  Workspace* W = nullptr;
+  WsLock lk;
+  SRS_TRY(acquire_ws(&W, &lk));
+  if (tmp) *tmp = W->tmp.p;
+  if (tmp_bytes) *tmp_bytes = W->tmp.bytes;
+  if (tmp2) *tmp2 = W->tmp2.p;
+  if (tmp2_bytes) *tmp2_bytes = W->tmp2.bytes;
+  return SRS_OK;
+}
+
 int srs_release_workspace(void) {
   release_host_stages();
   {
-    std::lock_guard<std::mutex> g(g_shmu);
+    std::lock_guard<std::mutex> g(g_split_mu);  // (waits for a running split)
     for (ShardBufs* B : g_shards) {
-      DevBuf* bufs[] = {&B->in, &B->part, &B->recv, &B->hist, &B->lut};
-      for (DevBuf* b : bufs)
-        if (b->p) (void)hipFree(b->p);
+      free_shard(B);
       delete B;
     }
     g_shards.clear();
   }
-  std::lock_guard<std::mutex> lk(g_wmu);
-  for (auto& kv : g_ws) {
-    Workspace* w = kv.second;
-    { std::lock_guard<std::mutex> busy(w->mu); }  // no call is using it any more
-    if (w->idle) {  // the last call's kernels may still read the buffers
-      (void)hipEventSynchronize(w->idle);
-      (void)hipEventDestroy(w->idle);
-    }
-    DevBuf* bufs[] = {&w->tmp, &w->tmp2, &w->stage, &w->desc, &w->big[0], &w->big[1], &w->local, &w->local2, &w->fallback, &w->fallback2, &w->redo, &w->shist, &w->lut, &w->lut_rbits,
-                      &w->copy, &w->plan, &w->tcount, &w->gcount, &w->tbase, &w->gbase,
-                      &w->var, &w->sbase, &w->tile_seg, &w->group_seg, &w->hist, &w->offs,
-                      &w->gsum, &w->gofs, &w->scan_tmp, &w->totals, &w->ctr,
-                      &w->prun, &w->ptile, &w->btot, &w->bnt, &w->btile, &w->nt_over, &w->gtile,
-                      &w->gorder};
-    for (DevBuf* b : bufs)
-      if (b->p) (void)hipFree(b->p);
-    for (auto& t : w->small_taken)
-      if (t.second.p) (void)hipFree(t.second.p);
-    (void)hipHostFree(w->h_ctr);
-    (void)hipHostFree(w->h_totals);
-    delete w;
+  std::map<int, std::shared_ptr<Workspace>> old;
+  {
+    std::lock_guard<std::mutex> lk(g_wmu);
+    old.swap(g_ws);
   }
-  g_ws.clear();
+  old.clear();  // each workspace is freed by its last holder (~Workspace)
   (void)hipGetLastError();
   return SRS_OK;
 }

@@ -79,6 +79,8 @@ bool launch_sample_hist16(const void* keys, int key_bytes, int elem_bytes, int64
 void launch_fill(int64_t n, int kind, uint64_t seed, uint64_t first, void* keys,
                  int npay, const Col* pays, hipStream_t st);
 void launch_set_desc(const SortDesc& d, SortDesc* out, hipStream_t st);
+// diagnostics: phase of each XCD's walk over its block range (xcd_remap)
+void set_xcd_rotation(int mode);
 // the copy list (finished segments not in OUT) home in one launch, column by
 // column with each buffer's stride (AoS slice columns back into records)
 // (chunks / cbase: nsegs u64 each; scan_temp: scan_temp_elems(nsegs) u64;

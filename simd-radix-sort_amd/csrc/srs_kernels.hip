@@ -589,11 +589,39 @@ __global__ void seg_map2_kernel(const int64_t* __restrict__ tbase, int64_t ntile
 // dealt round-robin over the 8 XCDs), so the partial cache lines that two
 // neighbouring tiles write into the same bucket meet in one L2. Bijective for
 // any grid size. Placement only affects speed, never results.
+// The OR of every thread's `v` into the workgroup's slots, one per wave:
+// each wave resets its own slot first (a wave's LDS operations take effect in
+// program order), so no block-wide reset has to be ordered before the other
+// waves' atomics. The caller barriers, then reads wave_or_read.
+template <int NW>
+__device__ __forceinline__ void wave_or_add(unsigned long long (&wor)[NW], uint32_t wave,
+                                            uint32_t lane, unsigned long long v) {
+  if (lane == 0) wor[wave] = 0;
+  if (v) atomicOr(&wor[wave], v);
+}
+template <int NW>
+__device__ __forceinline__ unsigned long long wave_or_read(const unsigned long long (&wor)[NW]) {
+  unsigned long long v = 0;
+#pragma unroll
+  for (int w = 0; w < NW; w++) v |= wor[w];
+  return v;
+}
+
+__device__ int g_xcd_rot;  // phase of each XCD's walk over its range (set_xcd_rotation)
+
 __device__ __forceinline__ int64_t xcd_remap(int64_t bid, int64_t nwg) {
   constexpr int64_t X = 8;
   const int64_t q = nwg / X, r = nwg % X;
   const int64_t xcd = bid % X, local = bid / X;
-  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + local;
+  const int64_t start = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  const int64_t len = xcd < r ? q + 1 : q;
+  const int m = g_xcd_rot;
+  int64_t l = local;
+  if (m == 1) l = (local + xcd * len / 8) % len;
+  else if (m == 2) l = (local + (xcd * 5 % 8) * len / 8 + (xcd * len) / 61) % len;
+  else if (m == 3 && (xcd & 1)) l = len - 1 - local;
+  else if (m == 4) l = (local + xcd * len / 16) % len;
+  return start + l;
 }
 
 // Partition passes: the digit table (2^lut_bits int32) is read once per
@@ -1679,7 +1707,7 @@ struct FastLds {
   uint16_t perm[NT * IT];                      // output slot -> original index
   uint16_t bin_start[(1 << kLocalTopBits) + 2];
   int maxlen;
-  unsigned long long sh_or;
+  unsigned long long wor[NT / 64];             // varying-bit OR, one slot per wave (wave_or)
   uint32_t hist2[(1 << kLocalTopBits) / 2];    // 16-bit bucket sizes, then cursors (pairs)
   uint32_t scan_sh[NT / 64 + 1];
 };
@@ -1705,7 +1733,6 @@ __device__ __forceinline__ bool local_fast_body(const SortDesc* __restrict__ des
   auto& hist2 = Ls.hist2;
   auto& bin_start = Ls.bin_start;
   auto& scan_sh = Ls.scan_sh;
-  auto& sh_or = Ls.sh_or;
   auto& maxlen = Ls.maxlen;
   const uint32_t wave = threadIdx.x >> 6;
   const uint32_t lane = lane_id();
@@ -1720,10 +1747,7 @@ __device__ __forceinline__ bool local_fast_body(const SortDesc* __restrict__ des
   STAMP_DECL
   STAMP();
 
-  if (threadIdx.x == 0) {
-    sh_or = 0;
-    maxlen = 0;
-  }
+  if (threadIdx.x == 0) maxlen = 0;  // (first used after several barriers)
   for (uint32_t i = threadIdx.x; i < (uint32_t)(NB / 2); i += NT) hist2[i] = 0;
 
   // ---- 1. keys (column 0 holds the key in its low bytes) -------------------
@@ -1750,9 +1774,9 @@ __device__ __forceinline__ bool local_fast_body(const SortDesc* __restrict__ des
   for (int k = 0; k < IT; k++)
     if (valid(k)) vor |= ukey(k) ^ uref;
   STAMP();  // 1: keys loaded
-  if (vor) atomicOr(&sh_or, (unsigned long long)vor);
+  wave_or_add(Ls.wor, wave, lane, (unsigned long long)vor);
   lds_barrier();
-  const unsigned long long var = sh_or;
+  const unsigned long long var = wave_or_read(Ls.wor);
 
   if (var != 0) {
     const int lo = __ffsll((long long)var) - 1;
@@ -2250,7 +2274,7 @@ struct DirectLds {
   uint64_t sbuf[NT * IT + kRankSortMax];      // sort words (+ sentinels), then the payloads
   uint32_t cur[(1 << kLocalTopBits) / 2 + 1];  // [0] = 0; bucket b: cur[1 + b/2], half b & 1
   uint32_t scan_sh[NT / 64 + 1];
-  unsigned long long sh_or;
+  unsigned long long wor[NT / 64];  // varying-bit OR, one slot per wave (wave_or_add)
   int maxlen;
 };
 
@@ -2288,10 +2312,7 @@ __global__ __launch_bounds__(NT, WPE) void local_direct_kernel(
   }
   Xform<U, false> xf;
   xf.init(*desc);
-  if (threadIdx.x == 0) {
-    Ls.sh_or = 0;
-    Ls.maxlen = 0;
-  }
+  if (threadIdx.x == 0) Ls.maxlen = 0;  // (first used after several barriers)
   for (uint32_t i = threadIdx.x; i < (uint32_t)(NB / 2 + 1); i += NT) cur[i] = 0;
 
   // ---- 1. keys ---------------------------------------------------------------
@@ -2305,11 +2326,11 @@ __global__ __launch_bounds__(NT, WPE) void local_direct_kernel(
 #pragma unroll
   for (int k = 0; k < IT; k++)
     if (valid(k)) vor |= ukey(k) ^ uref;
-  if (vor) atomicOr(&Ls.sh_or, (unsigned long long)vor);
+  wave_or_add(Ls.wor, wave, lane, (unsigned long long)vor);
   lds_barrier();
   // (LDS values made provably uniform: everything derived from them then
   // lives in SGPRs, not in the 128 VGPRs)
-  const unsigned long long var_l = Ls.sh_or;
+  const unsigned long long var_l = wave_or_read(Ls.wor);
   const unsigned long long var =
       ((unsigned long long)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(var_l >> 32))
        << 32) |
@@ -2618,12 +2639,14 @@ __device__ __forceinline__ bool local_stable_body(const SortDesc* __restrict__ d
   const uint64_t kmask = kbytes == 8 ? ~0ull : ((1ull << (8 * kbytes)) - 1);
   const int cnt = (int)g.len;
   const int64_t base = g.start;
-  __syncthreads();  // the previous segment is done with the shared arrays
-
+  // (reset before the barrier: the previous segment read them long before
+  // its last barrier, and this segment's atomics come after this one)
   if (threadIdx.x == 0) {
     sh_or = 0;
     maxlen = 0;
   }
+  __syncthreads();  // the previous segment is done with the shared arrays
+
   for (uint32_t i = threadIdx.x; i < (uint32_t)WCP; i += NT) wc_perm[i] = 0;
   for (uint32_t i = threadIdx.x; i < (uint32_t)NB; i += NT) bflag[i] = 0;
 
@@ -2909,8 +2932,8 @@ __device__ __forceinline__ void local_lsd_body(const SortDesc* __restrict__ desc
   {
     const int cnt = (int)g.len;
     const int64_t base = g.start;
+    if (threadIdx.x == 0) sh_or = 0;  // (before the barrier, as in local_stable_body)
     __syncthreads();
-    if (threadIdx.x == 0) sh_or = 0;
     U u[IT];
     uint32_t id[IT];
     bool valid[IT];
@@ -3450,6 +3473,13 @@ void launch_copy_list(const SortDesc* d, const Seg* segs, int64_t nsegs, uint64_
   copy_chunks_kernel<<<(unsigned)((nsegs + 255) / 256), 256, 0, st>>>(segs, nsegs, chunks);
   launch_excl_scan(chunks, cbase, nsegs, scan_temp, total, st);
   copy_list_kernel<<<kCopyGrid, 256, 0, st>>>(d, segs, nsegs, cbase, total);
+}
+
+void set_xcd_rotation(int mode) {
+  static int cur = 0;
+  if (mode == cur) return;
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(g_xcd_rot), &mode, sizeof(int));
+  cur = mode;
 }
 
 void launch_set_desc(const SortDesc& d, SortDesc* out, hipStream_t st) {

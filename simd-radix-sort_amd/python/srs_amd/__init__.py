@@ -88,6 +88,10 @@ def lib() -> ctypes.CDLL:
     L.srs_kernel_stats.argtypes = [ctypes.c_char_p, ctypes.POINTER(i64),
                                    ctypes.POINTER(ctypes.c_double),
                                    ctypes.POINTER(ctypes.c_double)]
+    L.srs_debug_alloc.argtypes = [ctypes.c_uint64, ctypes.c_int, ctypes.POINTER(vp)]
+    L.srs_debug_free.argtypes = [vp]
+    L.srs_debug_workspace.argtypes = [ctypes.POINTER(vp), ctypes.POINTER(ctypes.c_uint64),
+                                      ctypes.POINTER(vp), ctypes.POINTER(ctypes.c_uint64)]
     _lib = L
     return L
 
@@ -380,6 +384,27 @@ def last_local_counts():
     c = (ctypes.c_int64 * 2)()
     _check(lib().srs_debug_last_local_counts(c))
     return int(c[0]), int(c[1])
+
+
+def debug_alloc(nbytes: int, mode: int = 0) -> int:
+    """Raw device allocation on the current device (srs_debug_alloc; mode 0
+    hipMalloc, 1 contiguous, 2 VMM at 1 GiB alignment): the address."""
+    p = ctypes.c_void_p()
+    _check(lib().srs_debug_alloc(int(nbytes), int(mode), ctypes.byref(p)))
+    return int(p.value)
+
+
+def debug_free(ptr: int) -> None:
+    _check(lib().srs_debug_free(ctypes.c_void_p(ptr)))
+
+
+def debug_workspace():
+    """(tmp address, bytes, tmp2 address, bytes) of the current device."""
+    a, b = ctypes.c_void_p(), ctypes.c_void_p()
+    na, nb = ctypes.c_uint64(), ctypes.c_uint64()
+    _check(lib().srs_debug_workspace(ctypes.byref(a), ctypes.byref(na), ctypes.byref(b),
+                                     ctypes.byref(nb)))
+    return int(a.value or 0), int(na.value), int(b.value or 0), int(nb.value)
 
 
 def release_workspace() -> None:

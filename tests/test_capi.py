@@ -126,3 +126,19 @@ def test_hot_kernels_keep_their_occupancy():
                 occ = 6  # digit-table (LUT) passes stage a 26 KB table in LDS
             assert r["Occupancy"] >= occ, (name, r)
     assert seen == set(need)
+
+
+def test_library_matches_the_sources():
+    """srs_version() carries the hash of the sources the library was built
+    from (simd-radix-sort_amd/Makefile SRC_HASH): a stale libsrs_amd.so
+    shipped with the tree fails here, on CPU and on the GPU box alike."""
+    import hashlib
+
+    import srs_amd
+    pkg = os.path.join(REPO, "simd-radix-sort_amd")
+    files = [os.path.join(pkg, "csrc", f) for f in ("srs_kernels.hip", "srs_api.hip",
+                                                    "srs_common.h", "srs_kernels.h")]
+    files.append(HEADER)
+    h = hashlib.sha256(b"".join(open(f, "rb").read() for f in files)).hexdigest()[:16]
+    v = srs_amd.version()
+    assert v.endswith("src:" + h), (v, h)
