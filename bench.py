@@ -50,8 +50,13 @@ def parse():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--n", type=float, default=1e9, help="keys per GPU")
     ap.add_argument("--config", default="c1", choices=sorted(CONFIGS))
-    ap.add_argument("--cpu-sample", type=float, default=2 ** 29,
-                    help="keys in the bounded CPU-baseline sample (0 = skip)")
+    ap.add_argument("--cpu-sample", type=float, default=1e9,
+                    help="keys of the headline config's CPU baseline (the reference on one "
+                         "host core; 1e9 = the config itself; 0 = skip)")
+    ap.add_argument("--cpu-sample-extra", type=float, default=2 ** 27,
+                    help="keys of the CPU-baseline sample of each 'extra' config (0 = skip)")
+    ap.add_argument("--cpu-warmup", type=int, default=1,
+                    help="untimed warmup sorts before the timed CPU-baseline sort")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--shard", action="store_true",
                     help="run the multi-GPU shard protocol even at one rank (RCCL, world 1)")
@@ -145,7 +150,46 @@ def kind_id(name):
 # ---------------------------------------------------------------------------
 # CPU baseline: the reference's own AVX-512 sort (oracle/_ref) on host cores
 # ---------------------------------------------------------------------------
-def cpu_baseline(cfg_name, n_sample):
+def _sm64(x, np):
+    x = x + np.uint64(0x9E3779B97F4A7C15)
+    x = (x ^ (x >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+    x = (x ^ (x >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return x ^ (x >> np.uint64(31))
+
+
+def host_workload(cfg_name, n, seed, keys=None, pays=None, chunk=1 << 26):
+    """The config's records on the host, by the device fill's generator
+    (srs_fill_synthetic_device: key = splitmix64(seed + i), payload c =
+    splitmix64(bits(key) ^ c * 0xD1B54A32D192ED03)), generated chunk by chunk
+    into `keys` / `pays` (allocated when None)."""
+    import numpy as np
+    kname, psizes, _, _ = CONFIGS[cfg_name]
+    if keys is None:
+        keys = np.empty(n, np.float32 if kname == "f32" else np.uint64)
+        pays = [np.empty(n, {4: np.uint32, 8: np.uint64}[s]) for s in psizes]
+    for a in range(0, n, chunk):
+        b = min(n, a + chunk)
+        h = _sm64(np.arange(a, b, dtype=np.uint64) + np.uint64(seed), np)
+        if kname == "f32":
+            k = ((h >> np.uint64(40)).astype(np.int32).astype(np.float32) *
+                 np.float32(1.0 / 8388608.0) - np.float32(1.0))
+            bits = k.view(np.uint32).astype(np.uint64)
+        else:
+            k = bits = h
+        keys[a:b] = k
+        for c, p in enumerate(pays):
+            p[a:b] = _sm64(bits ^ np.uint64((c * 0xD1B54A32D192ED03) & 0xFFFFFFFFFFFFFFFF),
+                           np).astype(p.dtype)
+    return keys, pays
+
+
+def cpu_baseline(cfg_name, n_sample, warmups=1):
+    """The reference's own sort (oracle/_ref: radixSort.hpp, AVX-512
+    BitSorterSIMD) on one host core, timed as its perf harness times it
+    (src/perf.hpp:28-89): `warmups` untimed sorts of other data of the same
+    shape (measureTimePerElementWithRepsAndWarmup: one warmup and one run at
+    n >= 2^22), then one sort timed with CLOCK_PROCESS_CPUTIME_ID around the
+    call only. Generated with the device fill's generator."""
     sys.path.insert(0, os.path.join(REPO, "tests"))
     import numpy as np
     from srs_testlib import (oracle_sort_aos, oracle_sort_soa, ref_lib, ref_sort_aos,
@@ -153,65 +197,62 @@ def cpu_baseline(cfg_name, n_sample):
     kname, psizes, layout, _ = CONFIGS[cfg_name]
     kind = {"u64": 6, "f32": 8, "u32": 4}[kname]
     n = int(n_sample)
-    # same generator as the device fill (srs_fill_synthetic_device)
-    idx = np.arange(n, dtype=np.uint64) + np.uint64(42 << 32)
-
-    def sm(x):
-        x = x + np.uint64(0x9E3779B97F4A7C15)
-        x = (x ^ (x >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
-        x = (x ^ (x >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
-        return x ^ (x >> np.uint64(31))
-    h = sm(idx)
-    del idx
-    if kname == "f32":
-        keys = ((h >> np.uint64(40)).astype(np.int32).astype(np.float32) *
-                np.float32(1.0 / 8388608.0) - np.float32(1.0))
-        bits = keys.view(np.uint32).astype(np.uint64)
-    else:
-        keys = h
-        bits = h
-    pays = [sm(bits ^ np.uint64((c * 0xD1B54A32D192ED03) & 0xFFFFFFFFFFFFFFFF)).astype(
-        {4: np.uint32, 8: np.uint64}[s]) for c, s in enumerate(psizes)]
-    del bits, h
     use_ref = ref_lib() is not None
-    cpu_ns = None
-    if layout == "aos":
-        rec = np.empty((n, 16), np.uint8)
-        rec[:, :8] = keys.view(np.uint8).reshape(n, 8)
-        rec[:, 8:] = pays[0].view(np.uint8).reshape(n, 8)
+    t_gen = time.perf_counter()
+    keys, pays = host_workload(cfg_name, n, 43 << 32)  # warmup data (another seed)
+    gen_s = time.perf_counter() - t_gen
+
+    def one_sort(keys, pays):
+        """(wall s, CPU ns) of one sort of the config's records."""
+        if layout == "aos":
+            rec = np.empty((n, 16), np.uint8)
+            rec[:, :8] = keys.view(np.uint8).reshape(n, 8)
+            rec[:, 8:] = pays[0].view(np.uint8).reshape(n, 8)
+            t0, c0 = time.perf_counter(), time.process_time()
+            (ref_sort_aos if use_ref else oracle_sort_aos)(kind, True, rec)
+            return time.perf_counter() - t0, (time.process_time() - c0) * 1e9
         t0 = time.perf_counter()
-        c0 = time.process_time()
-        (ref_sort_aos if use_ref else oracle_sort_aos)(kind, True, rec)
-        cpu_ns = (time.process_time() - c0) * 1e9
-    elif use_ref:
-        t0 = time.perf_counter()
-        # CLOCK_PROCESS_CPUTIME_ID around the sort call only (src/perf.hpp:33-46)
-        cpu_ns = ref_sort_soa_timed(kind, True, keys, pays)
-    else:
-        t0 = time.perf_counter()
-        c0 = time.process_time()
-        oracle_sort_soa(kind, True, keys, pays)
-        cpu_ns = (time.process_time() - c0) * 1e9
-    dt = time.perf_counter() - t0
+        if use_ref:  # CLOCK_PROCESS_CPUTIME_ID around the sort call only (src/perf.hpp:33-46)
+            ns = ref_sort_soa_timed(kind, True, keys, pays)
+        else:
+            c0 = time.process_time()
+            oracle_sort_soa(kind, True, keys, pays)
+            ns = (time.process_time() - c0) * 1e9
+        return time.perf_counter() - t0, ns
+
+    warm = []
+    for w in range(warmups):
+        if w:
+            host_workload(cfg_name, n, (43 + w) << 32, keys, pays)
+        warm.append(round(one_sort(keys, pays)[0], 2))
+    host_workload(cfg_name, n, 42 << 32, keys, pays)  # the timed data: the bench's own input
+    dt, cpu_ns = one_sort(keys, pays)
+    del keys, pays
     try:
         model = [l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo")
                  if l.startswith("model name")][0]
     except Exception:
         model = platform.processor()
+    full = n == int(1e9)
     return {
-        "value": n / dt / 1e9,
+        "value": n / (cpu_ns / 1e9) / 1e9,
         "unit": "Gkeys/s",
         "cores": 1,
         "kind": "reference" if use_ref else "port",
         "cpu_time_s": round(cpu_ns / 1e9, 3),
-        "value_cpu_time": n / (cpu_ns / 1e9) / 1e9,
-        "sample": (f"bounded sample, not the 1e9 config: {n} keys of the same {cfg_name} "
-                   f"workload (same generator), one sort, {dt:.2f} s wall / "
-                   f"{cpu_ns / 1e9:.2f} s CLOCK_PROCESS_CPUTIME_ID, single-threaded on 1 core "
-                   f"of '{model}' (nproc={os.cpu_count()}); reference = jonicho radixSort.hpp "
-                   f"BitSorterSIMD AVX-512" if use_ref else
-                   f"bounded sample: {n} keys, C restatement (host lacks AVX-512 VBMI2), "
-                   f"{dt:.2f} s"),
+        "wall_s": round(dt, 3),
+        "value_wall": n / dt / 1e9,
+        "warmup_wall_s": warm,
+        "sample": (f"{'the full config' if full else 'bounded sample'}: {n} keys of the "
+                   f"{cfg_name} workload (the bench's generator and seed), {warmups} untimed "
+                   f"warmup sort(s) of other data of the same shape, then one sort timed with "
+                   f"CLOCK_PROCESS_CPUTIME_ID around the call (src/perf.hpp:28-89): "
+                   f"{cpu_ns / 1e9:.2f} s CPU, {dt:.2f} s wall; single-threaded on 1 core of "
+                   f"'{model}' (nproc={os.cpu_count()}); data generation {gen_s:.1f} s "
+                   f"(not timed); " +
+                   ("reference = jonicho radixSort.hpp BitSorterSIMD AVX-512, compiled from "
+                    "/root/reference by oracle/Makefile" if use_ref else
+                    "C restatement (host lacks AVX-512 VBMI2)")),
     }
 
 
@@ -283,7 +324,7 @@ def main():
     cpu = None
     if rank == 0 and args.cpu_sample > 0 and (world == 1):
         try:
-            cpu = cpu_baseline(args.config, args.cpu_sample)
+            cpu = cpu_baseline(args.config, min(args.cpu_sample, args.n), args.cpu_warmup)
         except Exception as e:  # report, never hide
             cpu = {"error": repr(e)}
 
@@ -295,6 +336,12 @@ def main():
                 r = measure(name, args, torch, srs_amd, dist, dev, rank, world, shard)
             except Exception as e:  # report, never hide
                 r = {"error": repr(e)}
+            if rank == 0 and args.cpu_sample_extra > 0 and "error" not in r:
+                try:
+                    r["cpu_baseline"] = cpu_baseline(name, min(args.cpu_sample_extra, args.n),
+                                                     args.cpu_warmup)
+                except Exception as e:  # report, never hide
+                    r["cpu_baseline"] = {"error": repr(e)}
             extra[name] = r
 
     if rank == 0:
