@@ -366,6 +366,8 @@ def main():
             "cpu_baseline": cpu,
             "verified": res["verified"],
         }
+        if res.get("phases") is not None:
+            out["phases"] = res["phases"]
         if extra:
             out["extra"] = extra
         print(json.dumps(out), flush=True)
@@ -459,6 +461,16 @@ def measure(cfg_name, args, torch, srs_amd, dist, dev, rank, world, shard):
         step()
     sync()
     ms_no_events = (time.perf_counter() - t2) / min(args.steps, 3) * 1e3
+    phases = None
+    if shard:
+        # per-rank phase stamps of the last step (HIP events), the bytes each
+        # rank sent to each peer, the implied link rate and the DESIGN.md §7
+        # model's prediction for those bytes
+        mine = sorter.phases()
+        mine["rank"] = rank
+        allph = [None] * world
+        dist.all_gather_object(allph, mine)
+        phases = allph
     if shard:
         tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -533,6 +545,7 @@ def measure(cfg_name, args, torch, srs_amd, dist, dev, rank, world, shard):
                         "total_ms_per_step": round(v["ms"] / args.steps, 3)}
                     for k, v in kstats.items()},
         "verified": verified,
+        **({"phases": phases} if phases is not None else {}),
     }
 
 

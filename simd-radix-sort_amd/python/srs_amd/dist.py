@@ -30,6 +30,8 @@ on MI355X under RCCL (HipShardOps, the product path). The reference
 """
 from __future__ import annotations
 
+import time
+
 import torch
 import torch.distributed as dist
 
@@ -58,6 +60,36 @@ def _comm(t):
     return t.view(_COMM_DT[t.element_size()])
 
 
+class PhaseClock:
+    """Stamps of one shard sort's phases: HIP events recorded on the stream
+    the phase runs on (read once the caller has synchronized), or host wall
+    time when the device is the CPU (the gloo tests)."""
+
+    def __init__(self, device):
+        self.cuda = torch.device(device).type == "cuda"
+        self.marks = []
+
+    def reset(self):
+        self.marks = []
+
+    def stamp(self, name, stream=None):
+        if self.cuda:
+            e = torch.cuda.Event(enable_timing=True)
+            e.record(stream)
+            self.marks.append((name, e))
+        else:
+            self.marks.append((name, time.perf_counter()))
+
+    def read(self):
+        """{name: ms since the first stamp}."""
+        if not self.marks:
+            return {}
+        t0 = self.marks[0][1]
+        if self.cuda:
+            return {n: round(t0.elapsed_time(e), 4) for n, e in self.marks}
+        return {n: round((t - t0) * 1e3, 4) for n, t in self.marks}
+
+
 class HipShardOps:
     """Device backend: the HIP kernels of libsrs_amd.so via the C ABI."""
 
@@ -79,14 +111,19 @@ class HipShardOps:
     def sort(self, keys, pays):
         self.srs.sort_device(keys, *pays, key_kind=self.kind)
 
-    def sort_segments(self, keys, pays, bounds, known_top_bits=0):
+    def sort_segments(self, keys, pays, bounds, known_top_bits=0, stamp=None):
         """Queue the sort of the given segments on a side stream, after the
-        work already queued on the current stream (the receives)."""
+        work already queued on the current stream (the receives). stamp(name,
+        stream) marks the start and end of the sort on that stream."""
         if self.stream is None:
             self.stream = torch.cuda.Stream(device=keys.device)
         self.stream.wait_stream(torch.cuda.current_stream(keys.device))
+        if stamp:
+            stamp("sort_start", self.stream)
         self.srs.sort_segments_device(keys, *pays, bounds=bounds, key_kind=self.kind,
                                       known_top_bits=known_top_bits, stream=self.stream)
+        if stamp:
+            stamp("sort_end", self.stream)
 
     def finish(self, device):
         if self.stream is not None:
@@ -126,6 +163,10 @@ class ShardSorter:
         self.recv_keys = torch.empty(cap, dtype=key_dtype, device=device)
         self.recv_pays = [torch.empty(cap, dtype=dt, device=device) for dt in payload_dtypes]
         self.last_counts = None
+        self.rec_bytes = (torch.empty(0, dtype=key_dtype).element_size() +
+                          sum(torch.empty(0, dtype=dt).element_size() for dt in payload_dtypes))
+        self.clock = PhaseClock(device)
+        self.last_bytes = None  # bytes this rank sent to each peer, per round
 
     def _ensure_capacity(self, total):
         if total <= self.recv_keys.numel():
@@ -161,11 +202,15 @@ class ShardSorter:
                               for p in self.part_pays]
         C = max(1, min(self.chunks, n))
         cb = [n * c // C for c in range(C + 1)]          # chunk c = input [cb[c], cb[c+1])
+        clk = self.clock
+        clk.reset()
+        clk.stamp("start")
         # 1-3: per-chunk histograms -> global histogram -> groups -> ranks
         hists = [self.ops.histogram(keys[cb[c]:cb[c + 1]], self.bits) for c in range(C)]
         hist = hists[0].clone()
         for h in hists[1:]:
             hist += h
+        clk.stamp("hist")
         dist.all_reduce(hist, group=self.group)
         group_of_bin, rank_of_group, first, last = self.plan(hist)
         # 4: every rank's group sizes per chunk (a group is a union of bins,
@@ -178,6 +223,7 @@ class ShardSorter:
         allcc = [torch.empty_like(cc) for _ in range(w)]
         dist.all_gather(allcc, cc, group=self.group)
         mat = [m.tolist() for m in allcc]                 # mat[src][chunk][g]
+        clk.stamp("plan")  # (after the host read of the all-gather: collectives done)
         counts = [sum(mat[me][c][g] for c in range(C)) for g in range(G)]
         owned = [[g for g in range(G) if rank_of_group[g] == r] for r in range(w)]
         # exchange round r of rank d moves d's groups owned[d][rg[d][r]]: a
@@ -277,13 +323,19 @@ class ShardSorter:
                 # expect this chunk's: keep to the agreed message plan (the
                 # buffers are sized by it) and fail on every rank at the end
                 bad = True
+            clk.stamp(f"partition{c}")
             if self.stage_host:  # the staged send buffers take the partitioned chunk
                 for (sb, _), (msb, _) in zip(cols, mcols):
                     msb[a:b].copy_(sb[a:b])
             pending += issue(0, [c])
+        # bytes this rank sends to each peer in each round (the link load)
+        self.last_bytes = [[0 if d == me else
+                            sum(piece(mat[me][c], d, r)[1] for c in range(C)) * self.rec_bytes
+                            for d in range(w)] for r in range(R)]
         for r in range(R):
             for req in pending:
                 req.wait()
+            clk.stamp(f"round{r}_recv")
             pending = issue(r + 1, range(C)) if r + 1 < R else []
             if self.stage_host:
                 land(r)
@@ -303,13 +355,16 @@ class ShardSorter:
                     bounds = [a]
                     for g in gs:
                         bounds.append(bounds[-1] + counts[g])
-                    self.ops.sort_segments(rk, rps, bounds, min(shared([g]) for g in gs))
+                    self.ops.sort_segments(rk, rps, bounds, min(shared([g]) for g in gs),
+                                           stamp=lambda nm, st, r=r: clk.stamp(f"round{r}_{nm}", st))
                 else:
                     # several sources (or chunks) interleave the groups: the
                     # round's key range is one segment (at w >= 2 its size
                     # needs no more levels than a group's would)
-                    self.ops.sort_segments(rk, rps, [a, b], shared(gs))
+                    self.ops.sort_segments(rk, rps, [a, b], shared(gs),
+                                           stamp=lambda nm, st, r=r: clk.stamp(f"round{r}_{nm}", st))
         self.ops.finish(self.device)
+        clk.stamp("end")
         # every rank learns whether any partition disagreed with the plan
         flag = torch.tensor([1 if bad else 0], dtype=torch.int64, device=hist.device)
         dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=self.group)
@@ -319,6 +374,39 @@ class ShardSorter:
         self.last_counts = (counts, [sum(mat[s][c][g] for c in range(C) for g in owned[me])
                                      for s in range(w)])
         return rk, rps
+
+    def phases(self, link_gbs_model=(50.0, 77.0)):
+        """The last sort's phase stamps (ms since its start; call after the
+        device is synchronized) and the link figures: bytes sent to each peer
+        per round, the busiest link's bytes over the exchange window (first
+        partition chunk done -> last round received) as the implied GB/s, and
+        what the DESIGN.md §7 model predicts for these bytes: the histogram
+        and plan, the first partition chunk, then the exchange at the given
+        per-link one-way rates, then the last round's sort."""
+        ph = self.clock.read()
+        out = {"stamps_ms": ph}
+        if self.last_bytes is None:
+            return out
+        R, w = len(self.last_bytes), self.world
+        per_peer = [sum(self.last_bytes[r][d] for r in range(R)) for d in range(w)]
+        busiest = max(per_peer) if per_peer else 0
+        out["bytes_to_peer_per_round"] = self.last_bytes
+        out["busiest_link_bytes"] = busiest
+        t_ex0 = ph.get("partition0")
+        t_ex1 = ph.get(f"round{R - 1}_recv")
+        if busiest and t_ex0 is not None and t_ex1 is not None and t_ex1 > t_ex0:
+            out["link_gbs"] = round(busiest / ((t_ex1 - t_ex0) * 1e-3) / 1e9, 2)
+        last_sort = None
+        if f"round{R - 1}_sort_end" in ph and f"round{R - 1}_sort_start" in ph:
+            last_sort = ph[f"round{R - 1}_sort_end"] - ph[f"round{R - 1}_sort_start"]
+        if t_ex0 is not None:
+            model = {}
+            for gbs in link_gbs_model:
+                ex = busiest / (gbs * 1e9) * 1e3
+                model[f"T_ms_at_{int(gbs)}GBs"] = round(t_ex0 + ex + (last_sort or 0.0), 3)
+            out["model"] = model
+            out["measured_T_ms"] = ph.get("end")
+        return out
 
     def _msgs(self, p2p, op, buf, off, cnt, peer):
         """One message per <= chunk_bytes piece (sender and receiver split a

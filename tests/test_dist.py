@@ -51,7 +51,9 @@ class NumpyShardOps:
         for p in pays:
             p.copy_(p[order])
 
-    def sort_segments(self, keys, pays, bounds, known_top_bits=0):
+    def sort_segments(self, keys, pays, bounds, known_top_bits=0, stamp=None):
+        if stamp:
+            stamp("sort_start", None)
         # the known prefix must really be shared inside every segment
         for a, b in zip(bounds[:-1], bounds[1:]):
             if b > a and known_top_bits:
@@ -59,6 +61,8 @@ class NumpyShardOps:
                 assert (top == top[0]).all()
         for a, b in zip(bounds[:-1], bounds[1:]):
             self.sort(keys[a:b], [p[a:b] for p in pays])
+        if stamp:
+            stamp("sort_end", None)
 
     def finish(self, device):
         pass
@@ -100,6 +104,7 @@ def _run(rank, world, kind, n_per, dist_kind, q, bits=8, chunks=4):
         # never more groups than histogram bins of the (clamped) key width
         assert sorter.groups <= 1 << sorter.bits
         ok, (op,) = sorter.sort(keys, [pay])
+        _check_phases(sorter, world, rank, n)
         mine = ok.numpy().copy()
         u = transformed_keys(kind, True, mine)
         sorted_ok = bool(np.all(u[1:] >= u[:-1]))
@@ -126,6 +131,30 @@ def _run(rank, world, kind, n_per, dist_kind, q, bits=8, chunks=4):
                    [b.tolist() for b in allb]))
         else:
             q.put((sorted_ok, True, True, None))
+
+
+def _check_phases(sorter, world, rank, n):
+    """bench.py's N > 1 line carries ShardSorter.phases() of every rank: the
+    stamps of each phase, the bytes sent to each peer per round, the implied
+    link rate and the DESIGN.md §7 model's prediction (JSON-serializable)."""
+    import json
+    ph = sorter.phases()
+    json.dumps(ph)
+    st = ph["stamps_ms"]
+    R = sorter.rounds
+    C = sorter.chunks
+    need = ["start", "hist", "plan", "end"] + [f"partition{c}" for c in range(C)] + \
+        [f"round{r}_recv" for r in range(R)]
+    assert all(k in st for k in need), (need, st)
+    assert st["start"] == 0 and all(v >= 0 for v in st.values())
+    assert st["plan"] >= st["hist"] and st["end"] >= st[f"round{R - 1}_recv"]
+    b = ph["bytes_to_peer_per_round"]
+    assert len(b) == R and all(len(x) == world and x[rank] == 0 for x in b)
+    tot = sum(sum(x) for x in b)
+    assert tot <= n * sorter.rec_bytes
+    assert ph["busiest_link_bytes"] == max(sum(x[d] for x in b) for d in range(world))
+    assert set(ph["model"]) == {"T_ms_at_50GBs", "T_ms_at_77GBs"}
+    assert ph["measured_T_ms"] == st["end"]
 
 
 def _run_world(world, kind, dist_kind, bits=8, chunks=4):
