@@ -501,10 +501,24 @@ constexpr int kGroups = kMaxBins;
 // *spread (also without a table): the sample's top 9 bits spread the keys
 // (no bucket above kBalancedSkew times its share), so a plain first digit
 // partitions them well.
+// *clusters (SoA only): the sampled keys form at most kMaxRanges clusters of
+// at most kClusterSpan adjacent 16-bit bins each (e.g. the reference's
+// Gaussian keys: one cluster around 0 for signed keys, two at both ends of
+// the range for unsigned ones): a range level decides (plan_range_level), no
+// digit table. Empty otherwise.
+struct KeyCluster {
+  int b0, b1;    // first and last sampled 16-bit bin
+  uint64_t cnt;  // sampled keys
+};
+constexpr int kClusterGap = 4096;  // bins between two clusters
+constexpr int kClusterSpan = 256;  // bins a cluster may cover
+
 int plan_balanced_level(Workspace* W, const Request& R, const SortDesc& d, bool* use,
-                        int* lut_entries, hipStream_t st, bool* spread) {
+                        int* lut_entries, hipStream_t st, bool* spread,
+                        std::vector<KeyCluster>* clusters) {
   *use = false;
   *spread = false;
+  clusters->clear();
   const int ks = key_size_of(R.kind);
   const int64_t n = R.num;
   if (R.nsegs > 0 || n < kBalancedMinN || ks < 4) return SRS_OK;
@@ -528,6 +542,21 @@ int plan_balanced_level(Workspace* W, const Request& R, const SortDesc& d, bool*
     top9max = std::max(top9max, t);
   }
   if (total == 0) return SRS_OK;
+  if (!R.aos) {
+    std::vector<KeyCluster> cl;
+    for (int b = 0; b < 65536; b++) {
+      if (!h[b]) continue;
+      if (cl.empty() || b - cl.back().b1 > kClusterGap) cl.push_back(KeyCluster{b, b, 0});
+      cl.back().b1 = b;
+      cl.back().cnt += h[b];
+    }
+    bool ok = (int)cl.size() <= kMaxRanges;
+    for (const KeyCluster& c : cl) ok &= c.b1 - c.b0 < kClusterSpan;
+    if (ok) {
+      *clusters = cl;
+      return SRS_OK;
+    }
+  }
   if (top9max * 512 <= (uint64_t)kBalancedSkew * total) {
     *spread = true;
     return SRS_OK;
@@ -615,6 +644,7 @@ struct LevelMode {
   const int32_t* nt_over = nullptr; // mode 2: tiles per segment
   const int32_t* torder = nullptr;  // mode 2: the count's tile order (stripe-major)
   int key_bits = 0;                 // mode 1
+  bool home = false;                // every bucket of this level is final: scatter to OUT
 };
 
 int run_level(Workspace* W, int ks, const SortDesc* d_desc, LevelState& S, int force_bits,
@@ -638,13 +668,14 @@ int run_level(Workspace* W, int ks, const SortDesc* d_desc, LevelState& S, int f
   if (small_plan) {
     TimedScope ts("plan", (double)nbig, st);
     launch_plan_small((Seg*)W->big[S.cur].p, nbig, plan, (int64_t*)W->tbase.p,
-                      (int64_t*)W->gbase.p, var, d_totals, &d_ctr->n_big, force_bits, S.tmp2,
-                      st, M.nt_over);
+                      (int64_t*)W->gbase.p, var, d_totals, &d_ctr->n_big, force_bits,
+                      S.tmp2 | (M.home ? 2 : 0), st, M.nt_over);
   } else {
     TimedScope ts("plan", (double)nbig, st);
     HIP_TRY(hipMemsetAsync(d_totals + 3, 0, sizeof(uint64_t), st));
     launch_plan((Seg*)W->big[S.cur].p, nbig, plan, (int64_t*)W->tcount.p,
-                (int64_t*)W->gcount.p, var, d_totals + 3, force_bits, S.tmp2, st, M.nt_over);
+                (int64_t*)W->gcount.p, var, d_totals + 3, force_bits, S.tmp2 | (M.home ? 2 : 0),
+                st, M.nt_over);
     launch_excl_scan((uint64_t*)W->tcount.p, (uint64_t*)W->tbase.p, nbig,
                      (uint64_t*)W->scan_tmp.p, d_totals + 0, st);
     launch_excl_scan((uint64_t*)W->gcount.p, (uint64_t*)W->gbase.p, nbig,
@@ -877,6 +908,99 @@ bool stripes_enabled() {
   return on;
 }
 
+// Range level: the keys form a few narrow clusters (the
+// sample's KeyClusters). One exact pass finds each cluster's smallest and
+// largest key (split points halfway between the sampled clusters); the first
+// level then sends key u of cluster c to bucket base_c + ((u - lo_c) >>
+// shift_c), lo_c = min_c rounded down to 2^shift_c, with the 512 buckets
+// shared out by the clusters' sizes and shift_c the smallest that fits. A
+// bucket's keys then share every bit above shift_c (its children's rbits):
+// Gaussian keys (~1200 values) take two levels and end single-valued in OUT,
+// instead of a level on the sign bit, count-only levels on shared bits and a
+// copy home. *final: every bucket holds one key value (shift 0 everywhere).
+// *one_value: all keys are equal.
+int plan_range_level(Workspace* W, const Request& R, const std::vector<KeyCluster>& cl,
+                     SortDesc& d, hipStream_t st, bool* use, bool* final_lvl, bool* one_value) {
+  *use = *final_lvl = *one_value = false;
+  const int ks = key_size_of(R.kind);
+  const int kb = 8 * ks;
+  const int K = (int)cl.size();
+  uint64_t hi[kMaxRanges] = {~0ull, ~0ull, ~0ull, ~0ull};
+  for (int k = 0; k + 1 < K; k++) {  // split halfway between the sampled clusters
+    const uint64_t mid_bin = ((uint64_t)cl[k].b1 + (uint64_t)cl[k + 1].b0 + 1) / 2;
+    hi[k] = (mid_bin << (kb - 16)) - 1;
+  }
+  SRS_TRY(ensure(W->totals, 2 * kMaxRanges * sizeof(uint64_t)));
+  unsigned long long* mm = (unsigned long long*)W->totals.p;
+  uint64_t init[2 * kMaxRanges];
+  for (int c = 0; c < kMaxRanges; c++) {
+    init[2 * c] = ~0ull;
+    init[2 * c + 1] = 0;
+  }
+  std::vector<uint64_t> got(2 * kMaxRanges);
+  HIP_TRY(hipMemcpyAsync(mm, init, sizeof init, hipMemcpyHostToDevice, st));
+  launch_key_minmax(R.in_cols[0], ks, ks, R.num, d.mpos, d.mneg, hi, mm, st);
+  HIP_TRY(hipMemcpyAsync(got.data(), mm, sizeof init, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  // the non-empty ranges (a range's keys: u in (hi[c-1], hi[c]])
+  struct Rg {
+    uint64_t mn, mx, cnt, hi;
+  };
+  std::vector<Rg> rg;
+  for (int c = 0; c < K; c++) {
+    if (got[2 * c] > got[2 * c + 1]) continue;  // no key fell into this range
+    rg.push_back(Rg{got[2 * c], got[2 * c + 1], std::max<uint64_t>(cl[c].cnt, 1), hi[c]});
+  }
+  if (rg.empty()) return SRS_OK;
+  if (rg.size() == 1 && rg[0].mn == rg[0].mx) {
+    *one_value = true;
+    return SRS_OK;
+  }
+  // one shift for every range: the smallest that fits all of them into the
+  // level's buckets (ranges keep their order: dense bucket bases)
+  const int R_ = (int)rg.size();
+  auto shr = [](uint64_t x, int s) { return s >= 64 ? 0 : x >> s; };
+  auto span = [&](int s) {
+    uint64_t t = 0;
+    for (const Rg& r : rg) t += shr(r.mx, s) - shr(r.mn, s) + 1;
+    return t;
+  };
+  int s = 0;
+  while (s < kb && span(s) > (uint64_t)kMaxBins) s++;
+  uint32_t used = 0;
+  for (int c = 0; c < kMaxRanges; c++) {
+    d.rng_hi[c] = ~0ull;
+    d.rng_adj[c] = 0;
+  }
+  std::vector<int> base(R_);
+  for (int c = 0; c < R_; c++) {
+    d.rng_hi[c] = c + 1 < R_ ? rg[c].hi : ~0ull;
+    base[c] = (int)used;
+    d.rng_adj[c] = used - (uint32_t)shr(rg[c].mn, s);  // (wrapping)
+    used += (uint32_t)(shr(rg[c].mx, s) - shr(rg[c].mn, s) + 1);
+  }
+  // children's rbits: the bits above the shift are shared in a bucket
+  std::vector<int32_t> rbits(kMaxBins, s);
+  SRS_TRY(ensure(W->lut_rbits, kMaxBins * sizeof(int32_t)));
+  HIP_TRY(hipMemcpyAsync(W->lut_rbits.p, rbits.data(), kMaxBins * sizeof(int32_t),
+                         hipMemcpyHostToDevice, st));
+  HIP_TRY(hipStreamSynchronize(st));  // (rbits goes out of scope)
+  d.digit_lut = nullptr;
+  d.lut_mode = 2;
+  d.lut_bits = kMaxDigitBits;
+  d.lut_shift = s;
+  d.lut_entries = 0;
+  *use = true;
+  *final_lvl = s == 0;
+  if (trace_levels())
+    for (int c = 0; c < R_; c++)
+      fprintf(stderr, "[srs] range %d: keys [%llx, %llx] -> buckets from %d, shift %d\n", c,
+              (unsigned long long)rg[c].mn, (unsigned long long)rg[c].mx, base[c], s);
+  return SRS_OK;
+}
+
+int copy_through(const Request& R, hipStream_t st);
+
 int run_sort(Workspace* W, const Request& R, hipStream_t st) {
   if (R.nsegs == 0 && R.num <= kLocalCap) return run_small(W, R, st);
   {
@@ -935,10 +1059,17 @@ int run_sort(Workspace* W, const Request& R, hipStream_t st) {
   d.stamp_acc = g_stamp_acc;
   d.lb_status = g_lb_status;
   d.lb_err = g_lb_err;
-  bool balanced = false, spread = false;
+  bool balanced = false, spread = false, ranges = false, ranges_final = false;
   int lut_entries = 0;
-  SRS_TRY(plan_balanced_level(W, R, d, &balanced, &lut_entries, st, &spread));
-  if (balanced) {
+  std::vector<KeyCluster> clusters;
+  SRS_TRY(plan_balanced_level(W, R, d, &balanced, &lut_entries, st, &spread, &clusters));
+  if (!clusters.empty()) {
+    bool one_value = false;
+    SRS_TRY(plan_range_level(W, R, clusters, d, st, &ranges, &ranges_final, &one_value));
+    if (one_value) return copy_through(R, st);  // (stable: nothing moves)
+    balanced = ranges;  // (the range level runs where a digit-table level would)
+  }
+  if (balanced && !ranges) {
     d.digit_lut = (const int32_t*)W->lut.p;
     d.lut_shift = d.key_bits - 16;
     d.lut_bits = 16;
@@ -1024,7 +1155,7 @@ int run_sort(Workspace* W, const Request& R, hipStream_t st) {
   // plain level skips a digit all keys share, a stripe level cannot (all-zero
   // keys: 9.4 ms plain, 17.7 ms with stripes), so the key sample decides.
   const bool stripes = R.nsegs == 0 && !d.canon_zero && (ks == 4 || ks == 8) &&
-                       (balanced || spread) &&
+                       (balanced || spread) && !ranges_final &&
                        n >= kStripeMinN && n < (int64_t(1) << 32) && n >= 2 * stripe_len &&
                        stripes_enabled();
   if (stripes) {
@@ -1068,8 +1199,10 @@ int run_sort(Workspace* W, const Request& R, hipStream_t st) {
   }
   if (balanced && !stripes && S.nbig > 0) {
     ++level;
+    LevelMode m0;
+    m0.home = ranges_final;  // (single-valued buckets: written home directly)
     SRS_TRY(run_level(W, ksl, d_desc, S, kMaxDigitBits, true, st,
-                      (const int32_t*)W->lut_rbits.p));
+                      (const int32_t*)W->lut_rbits.p, m0));
   }
   while (S.nbig > 0) {
     if (++level > 80) return fail(SRS_ERR_INTERNAL, "level limit exceeded");

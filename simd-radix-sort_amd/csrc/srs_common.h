@@ -62,8 +62,14 @@ struct SortDesc {
   const int32_t* digit_lut;
   int32_t lut_shift;
   int32_t lut_bits;   // mode 0: table size 2^lut_bits; staged in LDS when <= kLdsLutBits
-  int32_t lut_mode;   // 0 flat int32 table, 1 two-level u16 table (see DigitLut)
+  int32_t lut_mode;   // 0 flat int32 table, 1 two-level u16 table, 2 key ranges (see DigitLut)
   int32_t lut_entries;  // mode 1: u16 entries (4096 + 16 per split bin)
+  // lut_mode 2 (range level): up to kMaxRanges clusters of
+  // keys; key u belongs to range c = #{k : u > rng_hi[k]} and goes to bucket
+  // (uint32)(u >> lut_shift) + rng_adj[c] (wrapping): the range's buckets are
+  // consecutive aligned blocks of 2^lut_shift key values
+  uint64_t rng_hi[4];
+  uint32_t rng_adj[4];
   unsigned long long* stamp_acc;  // diagnostic builds only (SRS_STAMPS)
   // diagnostic builds only (SRS_DIAG_LOOKBACK): per (tile, digit) look-back
   // status words of the scatter and error counters [mismatch, timeout, hops]
@@ -161,6 +167,7 @@ constexpr int kMaxBins = 1 << kMaxDigitBits;   // histogram row stride (tile-maj
 static_assert(kScatterThreads >= kMaxBins, "the scatter tile scan gives one bin per thread");
 constexpr int kScanGroup = 256;                 // tiles per column-scan group
 constexpr int kHistMaxBits = 12;                // srs_key_histogram_device
+constexpr int kMaxRanges = 4;                   // key clusters of a range level (lut_mode 2)
 constexpr int kLdsLutBits = 12;                 // flat digit tables up to 4096 entries live in LDS
 constexpr int kLdsLutEntries = 4096 + 16 * 512; // two-level table worst case (24 KB of u16)
 // sampled 16-bit skew histogram (balanced first level): workgroups, and the

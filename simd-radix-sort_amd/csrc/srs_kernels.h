@@ -73,6 +73,8 @@ void launch_small_sort(int key_size, const SortDesc& d, Seg g, int64_t* taken, h
 void launch_local_lsd(int key_size, const SortDesc* d, const Seg* segs,
                       const unsigned long long* nsegs, int grid, hipStream_t st);
 int64_t sample_partial_bytes();
+void launch_key_minmax(const void* keys, int key_bytes, int elem_bytes, int64_t n, uint64_t mpos,
+                       uint64_t mneg, const uint64_t* hi, unsigned long long* mm, hipStream_t st);
 bool launch_sample_hist16(const void* keys, int key_bytes, int elem_bytes, int64_t n,
                           int64_t stride, int chunk, int64_t blocks, uint64_t mpos, uint64_t mneg,
                           uint32_t* partial, uint32_t* hist, hipStream_t st);

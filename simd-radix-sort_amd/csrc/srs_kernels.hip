@@ -250,11 +250,13 @@ __device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63; }
 //   mode 1: two-level: entry t = [u >> (shift + 4)] of a 4096-entry table;
 //           if t has bit 15 set, the group is [4096 + (t & 0x7fff) * 16 +
 //           ((u >> shift) & 15)] (a 12-bit bin split between groups).
+//   mode 2: key ranges (SortDesc::rng_*): no table, a few compares.
 struct DigitLut {
   const uint16_t* s;  // LDS copy, or null
   const int32_t* g;   // global flat table (mode 0 only, when s is null)
   int shift;
   int mode;
+  const SortDesc* r;   // mode 2: the key ranges (SortDesc::rng_*)
 };
 
 // Digit of a transformed key for a global pass: the key's bits
@@ -262,6 +264,14 @@ struct DigitLut {
 template <bool LUT, typename U>
 __device__ __forceinline__ uint32_t pass_digit(U u, int shift, uint32_t mask, const DigitLut& L) {
   if constexpr (LUT) {
+    if (L.mode == 2) {  // range c = #{k : u > hi_k} (unused ranges: hi = ~0)
+      const uint64_t v = (uint64_t)u;
+      const SortDesc* d = L.r;
+      const uint32_t a = v > d->rng_hi[2] ? d->rng_adj[3]
+                       : v > d->rng_hi[1] ? d->rng_adj[2]
+                       : v > d->rng_hi[0] ? d->rng_adj[1] : d->rng_adj[0];
+      return (uint32_t)(v >> L.shift) + a;
+    }
     const uint64_t x = (uint64_t)u >> L.shift;
     if (L.mode == 1) {
       const uint32_t t = L.s[x >> 4];
@@ -462,8 +472,12 @@ __device__ __forceinline__ void wlms_rank(const uint32_t (&dig)[ITEMS],
 // (choose_bits: srs_common.h, shared with the host)
 
 // nt_over (gathered level): the segment's tile count from its tile table
+// tmp2: bit 0 SortDesc::tmp2, bit 1 the level's buckets are all final (a
+// range level of single-valued buckets: scatter them home)
 __device__ __forceinline__ SegPlan make_plan(const Seg& g, int force_bits, int tmp2,
                                              const int32_t* nt_over = nullptr, int64_t s = 0) {
+  const bool home = (tmp2 & 2) != 0;
+  tmp2 &= 1;
   SegPlan p;
   p.start = g.start;
   p.len = g.len;
@@ -480,6 +494,10 @@ __device__ __forceinline__ SegPlan make_plan(const Seg& g, int force_bits, int t
   // writes the records home
   if (tmp2) p.dst = (g.buf == BUF_TMP) ? BUF_TMP2 : BUF_TMP;
   else p.dst = (g.buf == BUF_TMP) ? BUF_OUT : BUF_TMP;
+  // a digit that takes every remaining bit leaves single-valued buckets,
+  // which are final: write them home directly (no copy list; e.g. two-valued
+  // keys, or the last level of a narrow key range)
+  if (!tmp2 && (home || (force_bits <= 0 && p.shift == 0)) && g.buf == BUF_IN) p.dst = BUF_OUT;
   p.skip = 0;
   p.tile_base = 0;
   p.group_base = 0;
@@ -631,14 +649,13 @@ __device__ __forceinline__ int64_t xcd_remap(int64_t bid, int64_t nwg) {
 // barriers before the first use). Returns the table to read.
 template <bool LUT, int NT>
 __device__ __forceinline__ DigitLut stage_lut(const SortDesc* desc, uint16_t* slut) {
-  DigitLut L{nullptr, nullptr, 0, 0};
+  DigitLut L{};
   if (!LUT) return L;
   L.shift = desc->lut_shift;
   L.mode = desc->lut_mode;
-  // 16-byte range-checked buffer loads, all in flight before any LDS store
-  // (a loop of 2-byte loads waited for each one: ~16-48 round trips per
-  // workgroup, and every LUT-level workgroup stages the table)
-  if (L.mode == 1) {
+  L.r = desc;
+  if (L.mode == 2) {  // key ranges: no table to stage
+  } else if (L.mode == 1) {
     const int n8 = (desc->lut_entries + 7) >> 3;  // 4096 + 16 per split bin (<= kLdsLutEntries)
     constexpr int K = (kLdsLutEntries / 8 + NT - 1) / NT;
     const __amdgpu_buffer_rsrc_t r = strip_rsrc((const char*)desc->digit_lut, (uint32_t)n8 * 16u);
@@ -3096,6 +3113,82 @@ __global__ __launch_bounds__(256) void sample_reduce_kernel(const uint32_t* __re
 }
 
 int64_t sample_partial_bytes() { return (int64_t)kSampleWGs * 32768 * 4; }
+
+// Exact smallest and largest transformed key of each of up to kMaxRanges
+// key clusters (range c = #{k : u > hi[k]}): the range level's plan
+// (DESIGN.md §2). mm[2c] / mm[2c + 1] must hold ~0 / 0 before the launch.
+constexpr int kMinMaxThreads = 256;
+__global__ __launch_bounds__(kMinMaxThreads) void key_minmax_kernel(
+    const char* __restrict__ keys, int key_bytes, int elem_bytes, int64_t n, uint64_t mpos,
+    uint64_t mneg, uint64_t hi0, uint64_t hi1, uint64_t hi2, unsigned long long* __restrict__ mm) {
+  constexpr int R = kMaxRanges;
+  __shared__ unsigned long long sh[2 * R][kMinMaxThreads / 64];
+  const int kb = 8 * key_bytes;
+  uint64_t lo[R], hi[R];
+#pragma unroll
+  for (int c = 0; c < R; c++) {
+    lo[c] = ~0ull;
+    hi[c] = 0;
+  }
+  auto add = [&](uint64_t bits) {
+    const uint64_t u = bits ^ (((bits >> (kb - 1)) & 1) ? mneg : mpos);
+    const int c = (u > hi0) + (u > hi1) + (u > hi2);
+#pragma unroll
+    for (int k = 0; k < R; k++) {
+      if (c == k) {
+        lo[k] = u < lo[k] ? u : lo[k];
+        hi[k] = u > hi[k] ? u : hi[k];
+      }
+    }
+  };
+  const int64_t step = (int64_t)gridDim.x * kMinMaxThreads;
+  int64_t i = (int64_t)blockIdx.x * kMinMaxThreads + threadIdx.x;
+  for (; i + 3 * step < n; i += 4 * step) {  // four loads in flight per thread
+    uint64_t b[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) b[k] = load_w(keys + (i + k * step) * elem_bytes, key_bytes);
+#pragma unroll
+    for (int k = 0; k < 4; k++) add(b[k]);
+  }
+  for (; i < n; i += step) add(load_w(keys + i * elem_bytes, key_bytes));
+#pragma unroll
+  for (int c = 0; c < R; c++) {
+    for (int o = 32; o > 0; o >>= 1) {
+      const uint64_t l2 = __shfl_xor(lo[c], o), h2 = __shfl_xor(hi[c], o);
+      lo[c] = l2 < lo[c] ? l2 : lo[c];
+      hi[c] = h2 > hi[c] ? h2 : hi[c];
+    }
+  }
+  const uint32_t wave = threadIdx.x >> 6;
+  if (lane_id() == 0) {
+#pragma unroll
+    for (int c = 0; c < R; c++) {
+      sh[2 * c][wave] = lo[c];
+      sh[2 * c + 1][wave] = hi[c];
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < 2 * R) {
+    const int j = threadIdx.x;
+    unsigned long long v = sh[j][0];
+    for (int w = 1; w < kMinMaxThreads / 64; w++) {
+      const unsigned long long x = sh[j][w];
+      v = (j & 1) ? (x > v ? x : v) : (x < v ? x : v);
+    }
+    if (j & 1) {
+      if (v) atomicMax(&mm[j], v);
+    } else if (v != ~0ull) {
+      atomicMin(&mm[j], v);
+    }
+  }
+}
+
+void launch_key_minmax(const void* keys, int key_bytes, int elem_bytes, int64_t n, uint64_t mpos,
+                       uint64_t mneg, const uint64_t* hi, unsigned long long* mm, hipStream_t st) {
+  const int64_t blocks = std::min<int64_t>(2048, (n + kMinMaxThreads - 1) / kMinMaxThreads);
+  key_minmax_kernel<<<(unsigned)std::max<int64_t>(1, blocks), kMinMaxThreads, 0, st>>>(
+      (const char*)keys, key_bytes, elem_bytes, n, mpos, mneg, hi[0], hi[1], hi[2], mm);
+}
 
 bool launch_sample_hist16(const void* keys, int key_bytes, int elem_bytes, int64_t n,
                           int64_t stride, int chunk, int64_t blocks, uint64_t mpos, uint64_t mneg,
