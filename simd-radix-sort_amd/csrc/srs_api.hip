@@ -514,9 +514,10 @@ constexpr int kClusterGap = 4096;  // bins between two clusters
 constexpr int kClusterSpan = 256;  // bins a cluster may cover
 
 int plan_balanced_level(Workspace* W, const Request& R, const SortDesc& d, bool* use,
-                        int* lut_entries, hipStream_t st, bool* spread,
+                        int* lut_entries, int* lut_mode, hipStream_t st, bool* spread,
                         std::vector<KeyCluster>* clusters) {
   *use = false;
+  *lut_mode = 1;
   *spread = false;
   clusters->clear();
   const int ks = key_size_of(R.kind);
@@ -594,6 +595,141 @@ int plan_balanced_level(Workspace* W, const Request& R, const SortDesc& d, bool*
     int bl = 0;
     while ((1 << bl) <= diff) bl++;
     rbits[g] = d.key_bits - (16 - bl);  // the group's keys share 16 - bl top bits
+  }
+  // Split table (DigitLut mode 3), where it balances about as well: each
+  // top-9-bit bin t gets 2^lg_t consecutive groups, the next lg_t key bits
+  // (uniform floats: one exponent's mantissas; no group spans two bins, so a
+  // group's keys are uniform below its prefix and the next level's digit
+  // splits them evenly). One 2 KB table and one lookup per key instead of the
+  // two-level 16-bit table (up to 24 KB staged per tile, two dependent lookups).
+  {
+    const int kb = d.key_bits;
+    std::vector<uint64_t> ct(512, 0), cnt1(kGroups, 0);
+    for (int t = 0; t < 512; t++)
+      for (int j = 0; j < 128; j++) ct[t] += h[t * 128 + j];
+    for (int b = 0; b < 65536; b++) cnt1[lut[b]] += h[b];
+    const uint64_t max1 = *std::max_element(cnt1.begin(), cnt1.end());
+    // bins worth less than one group share groups (consecutive, until their
+    // keys add up to one group's share): the tails of a float distribution
+    // would otherwise take a group per exponent
+    std::vector<int> lg(512, -1);     // own groups 2^lg; -1: none
+    std::vector<int> share(512, -1);  // >= 0: index of the shared group it joins
+    std::vector<uint64_t> shared_cnt;
+    int S = 0;
+    {
+      double acc = 0;
+      bool open = false;
+      for (int t = 0; t < 512; t++) {
+        if (!ct[t]) continue;
+        const double x = 512.0 * (double)ct[t] / (double)total;
+        if (x < 1.0) {
+          if (!open) {
+            shared_cnt.push_back(0);
+            S++;
+            open = true;
+            acc = 0;
+          }
+          share[t] = (int)shared_cnt.size() - 1;
+          shared_cnt.back() += ct[t];
+          acc += x;
+          if (acc >= 1.0) open = false;
+          continue;
+        }
+        open = false;
+        int l = 0;
+        while (l < 9 && (double)(2 << l) <= x) l++;
+        lg[t] = l;
+        S += 1 << l;
+      }
+    }
+    auto gsize = [&](int t, int l) { return (double)ct[t] / (double)(1 << l); };
+    while (S > 512) {  // over budget: halve where the resulting groups stay smallest
+      int best = -1;
+      for (int t = 0; t < 512; t++)
+        if (lg[t] > 0 && (best < 0 || gsize(t, lg[t] - 1) < gsize(best, lg[best] - 1))) best = t;
+      if (best < 0) break;
+      S -= 1 << (lg[best] - 1);
+      lg[best]--;
+    }
+    while (true) {  // spare budget: split the largest groups further
+      int best = -1;
+      for (int t = 0; t < 512; t++)
+        if (lg[t] >= 0 && lg[t] < 9 && (best < 0 || gsize(t, lg[t]) > gsize(best, lg[best])))
+          best = t;
+      if (best < 0 || S + (1 << lg[best]) > 512) break;
+      S += 1 << lg[best];
+      lg[best]++;
+    }
+    // predicted largest group (exact from the 16-bit bins while lg <= 7)
+    uint64_t max3 = 0;
+    for (uint64_t c : shared_cnt) max3 = std::max(max3, c);
+    for (int t = 0; t < 512; t++) {
+      if (lg[t] < 0) continue;
+      if (lg[t] <= 7) {
+        const int per = 128 >> lg[t];
+        for (int g = 0; g < (1 << lg[t]); g++) {
+          uint64_t c = 0;
+          for (int j = 0; j < per; j++) c += h[t * 128 + g * per + j];
+          max3 = std::max(max3, c);
+        }
+      } else {
+        max3 = std::max(max3, (ct[t] + (1u << lg[t]) - 1) >> lg[t]);
+      }
+    }
+    if (S <= 512 && max3 * 4 <= max1 * 5) {
+      // entry t: first group (bits 0..15) | lg (16..23); an empty bin joins
+      // the group before it (or the first group)
+      std::vector<int32_t> tab(512);
+      std::vector<uint64_t> glo(kGroups, ~0ull), ghi(kGroups, 0);
+      const int unit = kb - 9;  // key bits below the top 9
+      int run = 0, cur_share = -1;
+      for (int t = 0; t < 512; t++) {
+        const uint64_t t0 = (uint64_t)t << unit;
+        const uint64_t tl = t0 + ((uint64_t(1) << unit) - 1);
+        if (lg[t] < 0) {  // a shared group (a new one when its index changes), or an
+          int g;          // empty bin joining the group before it
+          if (share[t] >= 0 && share[t] != cur_share) {
+            cur_share = share[t];
+            g = run++;
+          } else {
+            g = run > 0 ? run - 1 : 0;
+          }
+          tab[t] = g;
+          glo[g] = std::min(glo[g], t0);
+          ghi[g] = std::max(ghi[g], tl);
+          continue;
+        }
+        tab[t] = run | (lg[t] << 16);
+        const int sub = unit - lg[t];
+        for (int j = 0; j < (1 << lg[t]); j++) {
+          const uint64_t a = t0 + ((uint64_t)j << sub);
+          glo[run + j] = std::min(glo[run + j], a);
+          ghi[run + j] = std::max(ghi[run + j], a + ((uint64_t(1) << sub) - 1));
+        }
+        run += 1 << lg[t];
+      }
+      for (int g = 0; g < kGroups; g++) {
+        if (glo[g] > ghi[g]) {
+          rbits[g] = kb;  // (no keys)
+          continue;
+        }
+        const uint64_t x = glo[g] ^ ghi[g];
+        rbits[g] = x ? 64 - __builtin_clzll(x) : 0;
+      }
+      SRS_TRY(ensure(W->lut, 512 * sizeof(int32_t)));
+      SRS_TRY(ensure(W->lut_rbits, kGroups * sizeof(int32_t)));
+      HIP_TRY(hipMemcpyAsync(W->lut.p, tab.data(), 512 * 4, hipMemcpyHostToDevice, st));
+      HIP_TRY(hipMemcpyAsync(W->lut_rbits.p, rbits.data(), rbits.size() * 4,
+                             hipMemcpyHostToDevice, st));
+      HIP_TRY(hipStreamSynchronize(st));  // the host vectors go out of scope
+      *lut_entries = 1024;  // (u16 units)
+      *lut_mode = 3;
+      *use = true;
+      if (trace_levels())
+        fprintf(stderr, "[srs] split table: %d groups, largest %llu vs %llu (16-bit table)\n", S,
+                (unsigned long long)max3, (unsigned long long)max1);
+      return SRS_OK;
+    }
   }
   // two-level u16 table (DigitLut mode 1): a 12-bit bin whose 16 sub-bins
   // fall into one group maps straight to it; a split bin points to 16 entries
@@ -1060,9 +1196,10 @@ int run_sort(Workspace* W, const Request& R, hipStream_t st) {
   d.lb_status = g_lb_status;
   d.lb_err = g_lb_err;
   bool balanced = false, spread = false, ranges = false, ranges_final = false;
-  int lut_entries = 0;
+  int lut_entries = 0, lut_mode = 1;
   std::vector<KeyCluster> clusters;
-  SRS_TRY(plan_balanced_level(W, R, d, &balanced, &lut_entries, st, &spread, &clusters));
+  SRS_TRY(plan_balanced_level(W, R, d, &balanced, &lut_entries, &lut_mode, st, &spread,
+                              &clusters));
   if (!clusters.empty()) {
     bool one_value = false;
     SRS_TRY(plan_range_level(W, R, clusters, d, st, &ranges, &ranges_final, &one_value));
@@ -1071,9 +1208,9 @@ int run_sort(Workspace* W, const Request& R, hipStream_t st) {
   }
   if (balanced && !ranges) {
     d.digit_lut = (const int32_t*)W->lut.p;
-    d.lut_shift = d.key_bits - 16;
-    d.lut_bits = 16;
-    d.lut_mode = 1;
+    d.lut_shift = d.key_bits - (lut_mode == 3 ? 9 : 16);
+    d.lut_bits = lut_mode == 3 ? 9 : 16;
+    d.lut_mode = lut_mode;
     d.lut_entries = lut_entries;
   }
   SRS_TRY(ensure(W->desc, sizeof(SortDesc)));

@@ -251,6 +251,8 @@ __device__ __forceinline__ uint32_t lane_id() { return threadIdx.x & 63; }
 //           if t has bit 15 set, the group is [4096 + (t & 0x7fff) * 16 +
 //           ((u >> shift) & 15)] (a 12-bit bin split between groups).
 //   mode 2: key ranges (SortDesc::rng_*): no table, a few compares.
+//   mode 3: split table, u32 entry [u >> shift] (top 9 bits) = first group |
+//           lg << 16: group = first + the next lg key bits.
 struct DigitLut {
   const uint16_t* s;  // LDS copy, or null
   const int32_t* g;   // global flat table (mode 0 only, when s is null)
@@ -273,6 +275,11 @@ __device__ __forceinline__ uint32_t pass_digit(U u, int shift, uint32_t mask, co
       return (uint32_t)(v >> L.shift) + a;
     }
     const uint64_t x = (uint64_t)u >> L.shift;
+    if (L.mode == 3) {  // split table: first group | lg << 16 per top-9-bit bin
+      const uint32_t e = ((const uint32_t*)L.s)[(uint32_t)x];
+      const uint32_t lg = e >> 16;
+      return (e & 0xFFFFu) + ((uint32_t)((uint64_t)u >> (L.shift - (int)lg)) & ((1u << lg) - 1u));
+    }
     if (L.mode == 1) {
       const uint32_t t = L.s[x >> 4];
       return (t & 0x8000u) ? L.s[4096 + ((t & 0x7fffu) << 4) + (uint32_t)(x & 15)] : t;
@@ -655,6 +662,12 @@ __device__ __forceinline__ DigitLut stage_lut(const SortDesc* desc, uint16_t* sl
   L.mode = desc->lut_mode;
   L.r = desc;
   if (L.mode == 2) {  // key ranges: no table to stage
+  } else if (L.mode == 3) {  // split table: 512 u32 entries (2 KB)
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    const __amdgpu_buffer_rsrc_t r = strip_rsrc((const char*)desc->digit_lut, 2048u);
+    for (uint32_t i = threadIdx.x; i < 128u; i += NT)
+      ((u32x4*)slut)[i] = __builtin_amdgcn_raw_buffer_load_b128(r, i * 16u, 0, 0);
+    L.s = slut;
   } else if (L.mode == 1) {
     const int n8 = (desc->lut_entries + 7) >> 3;  // 4096 + 16 per split bin (<= kLdsLutEntries)
     constexpr int K = (kLdsLutEntries / 8 + NT - 1) / NT;
