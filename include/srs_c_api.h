@@ -263,6 +263,18 @@ int srs_debug_alloc(uint64_t bytes, int mode, void** ptr);
 int srs_debug_free(void* ptr);
 int srs_debug_workspace(void** tmp, uint64_t* tmp_bytes, void** tmp2, uint64_t* tmp2_bytes);
 
+/* The balanced first level's digit table, planned on the host from a
+ * 65536-bin histogram of the top 16 transformed key bits (the sample the
+ * sort takes of large inputs) for `num` input keys of key_bits (32 / 64):
+ * *mode 0 (no table), 1 (table = 65536 group ids, one per 16-bit bin) or 3
+ * (table = 512 split entries: first group | lg << 16 per top-9-bit bin);
+ * rbits = 512 per-group unsorted bit counts; *overflow = keys the next
+ * level is predicted to leave above the LDS capacity (overflow_other: for
+ * the other table). Host only (no GPU); tests check the plan with it. */
+int srs_debug_plan_table(const uint32_t* hist, int64_t num, int key_bits, int32_t* mode,
+                         int32_t* groups, double* overflow, double* overflow_other,
+                         int32_t* table, int32_t* rbits);
+
 /* Release cached device workspaces (for leak checks / shutdown). */
 int srs_release_workspace(void);
 

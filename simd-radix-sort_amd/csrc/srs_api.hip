@@ -501,6 +501,301 @@ constexpr int kGroups = kMaxBins;
 // *spread (also without a table): the sample's top 9 bits spread the keys
 // (no bucket above kBalancedSkew times its share), so a plain first digit
 // partitions them well.
+// The digit table of a balanced first level, planned from the sampled
+// 16-bit histogram h of the transformed keys (n input keys): mode 0 (no
+// table: it would not beat the plain digit), 1 (16-bit bins -> groups,
+// lut16) or 3 (split table, tab3), each group's rbits, and the predicted
+// keys the next level leaves above the LDS capacity (over; over_other for
+// the table not taken). Host only; srs_debug_plan_table exposes it.
+struct TablePlan {
+  int mode = 0;
+  std::vector<int32_t> lut16, tab3, rbits;
+  int groups = 0;
+  double over = 0, over_other = 0;
+};
+
+void plan_table(const std::vector<uint32_t>& h, int64_t n, int key_bits, TablePlan* P) {
+  *P = TablePlan();
+  uint64_t total = 0;
+  for (uint32_t v : h) total += v;
+  if (total == 0) return;
+  // Bins -> groups. Candidate groupings of the 16-bit bins into 512 key-range
+  // groups; the one whose next level is predicted to leave the fewest keys in
+  // buckets above the LDS capacity wins (a group's next digit splits its key
+  // range evenly, so a group that mixes bins of different key density, e.g.
+  // two float exponents, overfills the buckets of the denser one: C2 had 2101
+  // such buckets, 5 % of its keys, taking a third and fourth level):
+  //  * cumulative: group of bin b = floor(G * (keys before b + half of b) / total);
+  //  * bin-aligned: a top-9-bit bin worth at least one group gets groups of its
+  //    own, cut at 16-bit bins by key counts; bins worth less share groups of
+  //    at most one share.
+  const double to_n = (double)n / (double)total;  // sample -> input keys
+  std::vector<uint64_t> ct(512, 0);
+  for (int t = 0; t < 512; t++)
+    for (int j = 0; j < 128; j++) ct[t] += h[t * 128 + j];
+  // predicted keys the next level leaves in buckets above kLocalCap (keys
+  // uniform inside a 16-bit bin), or that need two more levels
+  auto overflow = [&](const std::vector<int32_t>& L) -> double {
+    std::vector<int32_t> fst(kGroups, -1), lst(kGroups, -1);
+    std::vector<uint64_t> cnt(kGroups, 0);
+    for (int b = 0; b < 65536; b++) {
+      const int g = L[b];
+      if (fst[g] < 0) fst[g] = b;
+      lst[g] = b;
+      cnt[g] += h[b];
+    }
+    double over = 0;
+    for (int g = 0; g < kGroups; g++) {
+      const double len = (double)cnt[g] * to_n;
+      if (len <= kLocalCap) continue;
+      int bl = 0;
+      while ((1 << bl) <= (fst[g] ^ lst[g])) bl++;
+      int need;
+      if (levels_for((int64_t)len, kLocalTarget, &need) > 1) {
+        over += len;
+        continue;
+      }
+      const int bits = choose_bits((int64_t)len, key_bits - (16 - bl));
+      if (bits >= bl) {  // each bin splits into 2^(bits - bl) buckets
+        for (int b = fst[g]; b <= lst[g]; b++)
+          if ((double)h[b] * to_n / (double)(1 << (bits - bl)) > kLocalCap) over += h[b] * to_n;
+      } else {  // each bucket spans 2^(bl - bits) bins of the aligned range
+        const int span = 1 << (bl - bits), b0 = fst[g] & ~((1 << bl) - 1);
+        for (int q = 0; q < (1 << bits); q++) {
+          double c = 0;
+          for (int b = std::max(fst[g], b0 + q * span); b < b0 + (q + 1) * span && b <= lst[g]; b++)
+            c += h[b];
+          if (c * to_n > kLocalCap) over += c * to_n;
+        }
+      }
+    }
+    return over;
+  };
+  std::vector<int32_t> lut(65536), first(kGroups, -1), last(kGroups, -1), rbits(kGroups);
+  {
+    double before = 0;
+    for (int b = 0; b < 65536; b++) {
+      int g = (int)((before + 0.5 * h[b]) * kGroups / (double)total);
+      g = std::min(std::max(g, b ? lut[b - 1] : 0), kGroups - 1);
+      lut[b] = g;
+      before += h[b];
+    }
+  }
+  double over_best = overflow(lut);
+  {
+    std::vector<int32_t> la(65536, 0);
+    std::vector<double> x(512);
+    for (int t = 0; t < 512; t++) x[t] = (double)kGroups * (double)ct[t] / (double)total;
+    for (double sc = 1.0; sc > 0.5; sc -= 0.005) {
+      std::vector<int> nt(512, 0);
+      int S = 0;
+      double acc = 0;
+      bool open = false;
+      for (int t = 0; t < 512; t++) {
+        if (!ct[t]) continue;
+        if (x[t] < 1.0) {
+          if (!open || acc + x[t] > 1.0) {
+            S++;
+            open = true;
+            acc = 0;
+          }
+          acc += x[t];
+          continue;
+        }
+        open = false;
+        nt[t] = std::min(128, std::max(1, (int)std::lround(x[t] * sc)));
+        S += nt[t];
+      }
+      if (S > kGroups) continue;
+      int g = -1;
+      acc = 0;
+      open = false;
+      for (int t = 0; t < 512; t++) {
+        if (!ct[t] || x[t] < 1.0) {
+          if (ct[t] && (!open || acc + x[t] > 1.0)) {
+            g++;
+            open = true;
+            acc = 0;
+          }
+          acc += x[t];
+          for (int j = 0; j < 128; j++) la[t * 128 + j] = std::max(g, 0);
+          continue;
+        }
+        open = false;
+        const int base = g + 1;
+        double before = 0;
+        int prev = 0;
+        for (int j = 0; j < 128; j++) {
+          const double hj = h[t * 128 + j];
+          int k = (int)((before + 0.5 * hj) * nt[t] / (double)ct[t]);
+          k = std::min(std::max(k, prev), nt[t] - 1);
+          prev = k;
+          la[t * 128 + j] = base + k;
+          before += hj;
+        }
+        g = base + nt[t] - 1;
+      }
+      const double o = overflow(la);
+      if (o <= over_best) {
+        over_best = o;
+        lut.swap(la);
+      }
+      break;
+    }
+  }
+  for (int b = 0; b < 65536; b++) {
+    const int g = lut[b];
+    if (first[g] < 0) first[g] = b;
+    last[g] = b;
+  }
+  // the table only pays when its groups outnumber the plain digit's
+  // non-empty buckets (Gaussian int64 keys fill two 16-bit bins: both ways
+  // give two buckets, and the table pass is the slower one)
+  int groups_used = 0, buckets_used = 0;
+  {
+    std::vector<uint8_t> has(kGroups, 0);
+    for (int b = 0; b < 65536; b++)
+      if (h[b]) has[lut[b]] = 1;
+    for (int g = 0; g < kGroups; g++) groups_used += has[g];
+  }
+  for (int b = 0; b < 512; b++) {
+    bool any = false;
+    for (int j = 0; j < 128 && !any; j++) any = h[b * 128 + j] != 0;
+    buckets_used += any;
+  }
+  if (groups_used < 2 * buckets_used) return;
+  for (int g = 0; g < kGroups; g++) {
+    const int diff = first[g] < 0 ? 0xFFFF : (first[g] ^ last[g]);
+    int bl = 0;
+    while ((1 << bl) <= diff) bl++;
+    rbits[g] = key_bits - (16 - bl);  // the group's keys share 16 - bl top bits
+  }
+  // Split table (DigitLut mode 3), when its next level overflows no more:
+  // each top-9-bit bin t gets 2^lg_t consecutive groups, the next lg_t key
+  // bits (no group spans two bins unless both are worth less than a group).
+  // One 2 KB table and one lookup per key instead of the two-level 16-bit
+  // table (up to 24 KB staged per tile, two dependent lookups).
+  {
+    const int kb = key_bits;
+    // bins worth less than one group share groups (consecutive, at most one
+    // share each): the tails of a float distribution would otherwise take a
+    // group per exponent
+    std::vector<int> lg(512, -1);     // own groups 2^lg; -1: none
+    std::vector<int> share(512, -1);  // >= 0: index of the shared group it joins
+    int S = 0;
+    {
+      double acc = 0;
+      int nsh = 0;
+      bool open = false;
+      for (int t = 0; t < 512; t++) {
+        if (!ct[t]) continue;
+        const double x = 512.0 * (double)ct[t] / (double)total;
+        if (x < 1.0) {
+          if (!open || acc + x > 1.0) {
+            nsh++;
+            S++;
+            open = true;
+            acc = 0;
+          }
+          share[t] = nsh - 1;
+          acc += x;
+          continue;
+        }
+        open = false;
+        int l = 0;
+        while (l < 9 && (double)(2 << l) <= x * 1.4142) l++;  // (nearest power of two)
+        lg[t] = l;
+        S += 1 << l;
+      }
+    }
+    auto gsize = [&](int t, int l) { return (double)ct[t] / (double)(1 << l); };
+    while (S > 512) {  // over budget: halve where the resulting groups stay smallest
+      int best = -1;
+      for (int t = 0; t < 512; t++)
+        if (lg[t] > 0 && (best < 0 || gsize(t, lg[t] - 1) < gsize(best, lg[best] - 1))) best = t;
+      if (best < 0) break;
+      S -= 1 << (lg[best] - 1);
+      lg[best]--;
+    }
+    while (true) {  // spare budget: split the largest groups that still fit
+      int best = -1;
+      for (int t = 0; t < 512; t++)
+        if (lg[t] >= 0 && lg[t] < 9 && S + (1 << lg[t]) <= 512 &&
+            (best < 0 || gsize(t, lg[t]) > gsize(best, lg[best])))
+          best = t;
+      if (best < 0) break;
+      S += 1 << lg[best];
+      lg[best]++;
+    }
+    // the same grouping at 16-bit resolution (representable while lg <= 7)
+    bool repr = S <= 512;
+    std::vector<int32_t> l3(65536, 0);
+    {
+      int run = 0, cur_share = -1;
+      for (int t = 0; t < 512 && repr; t++) {
+        if (lg[t] < 0) {
+          int g;
+          if (share[t] >= 0 && share[t] != cur_share) {
+            cur_share = share[t];
+            g = run++;
+          } else {
+            g = run > 0 ? run - 1 : 0;
+          }
+          for (int j = 0; j < 128; j++) l3[t * 128 + j] = g;
+          continue;
+        }
+        if (lg[t] > 7) {
+          repr = false;
+          break;
+        }
+        for (int j = 0; j < 128; j++) l3[t * 128 + j] = run + (j >> (7 - lg[t]));
+        run += 1 << lg[t];
+      }
+    }
+    const double over3 = repr ? overflow(l3) : 1e300;
+    if (repr && over3 <= over_best) {
+      // entry t: first group (bits 0..15) | lg (16..23); shared and empty
+      // bins: the group (lg 0)
+      std::vector<int32_t> tab(512);
+      std::vector<uint64_t> glo(kGroups, ~0ull), ghi(kGroups, 0);
+      const int unit = kb - 9;  // key bits below the top 9
+      for (int t = 0; t < 512; t++) {
+        const uint64_t t0 = (uint64_t)t << unit;
+        const int l = lg[t] < 0 ? 0 : lg[t];
+        const int g0 = l3[t * 128];
+        tab[t] = g0 | (l << 16);
+        const int sub = unit - l;
+        for (int j = 0; j < (1 << l); j++) {
+          const uint64_t a0 = t0 + ((uint64_t)j << sub);
+          glo[g0 + j] = std::min(glo[g0 + j], a0);
+          ghi[g0 + j] = std::max(ghi[g0 + j], a0 + ((uint64_t(1) << sub) - 1));
+        }
+      }
+      for (int g = 0; g < kGroups; g++) {
+        if (glo[g] > ghi[g]) {
+          rbits[g] = kb;  // (no keys)
+          continue;
+        }
+        const uint64_t x = glo[g] ^ ghi[g];
+        rbits[g] = x ? 64 - __builtin_clzll(x) : 0;
+      }
+      P->mode = 3;
+      P->tab3 = tab;
+      P->rbits = rbits;
+      P->groups = S;
+      P->over = over3;
+      P->over_other = over_best;
+      return;
+    }
+    P->over_other = over3;
+  }
+  P->mode = 1;
+  P->lut16 = lut;
+  P->rbits = rbits;
+  P->groups = groups_used;
+  P->over = over_best;
+}
+
 // *clusters (SoA only): the sampled keys form at most kMaxRanges clusters of
 // at most kClusterSpan adjacent 16-bit bins each (e.g. the reference's
 // Gaussian keys: one cluster around 0 for signed keys, two at both ends of
@@ -563,174 +858,26 @@ int plan_balanced_level(Workspace* W, const Request& R, const SortDesc& d, bool*
     return SRS_OK;
   }
   if (R.aos) return SRS_OK;  // (the digit table is not used for AoS records)
-  // bins -> groups: group of bin b = floor(G * (keys before b + half of b) / total)
-  std::vector<int32_t> lut(65536), first(kGroups, -1), last(kGroups, -1), rbits(kGroups);
-  double before = 0;
-  for (int b = 0; b < 65536; b++) {
-    int g = (int)((before + 0.5 * h[b]) * kGroups / (double)total);
-    g = std::min(std::max(g, b ? lut[b - 1] : 0), kGroups - 1);
-    lut[b] = g;
-    if (first[g] < 0) first[g] = b;
-    last[g] = b;
-    before += h[b];
+  TablePlan P;
+  plan_table(h, n, d.key_bits, &P);
+  if (trace_levels() && P.mode)
+    fprintf(stderr, "[srs] digit table mode %d: %d groups, predicted overflow %.0f keys (other "
+            "table %.0f)\n", P.mode, P.groups, P.over, P.over_other);
+  if (P.mode == 0) return SRS_OK;
+  std::vector<int32_t>& rbits = P.rbits;
+  if (P.mode == 3) {
+    SRS_TRY(ensure(W->lut, 512 * sizeof(int32_t)));
+    SRS_TRY(ensure(W->lut_rbits, kGroups * sizeof(int32_t)));
+    HIP_TRY(hipMemcpyAsync(W->lut.p, P.tab3.data(), 512 * 4, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(W->lut_rbits.p, rbits.data(), rbits.size() * 4, hipMemcpyHostToDevice,
+                           st));
+    HIP_TRY(hipStreamSynchronize(st));  // the host vectors go out of scope
+    *lut_entries = 1024;  // (u16 units)
+    *lut_mode = 3;
+    *use = true;
+    return SRS_OK;
   }
-  // the table only pays when its groups outnumber the plain digit's
-  // non-empty buckets (Gaussian int64 keys fill two 16-bit bins: both ways
-  // give two buckets, and the table pass is the slower one)
-  int groups_used = 0, buckets_used = 0;
-  {
-    std::vector<uint8_t> has(kGroups, 0);
-    for (int b = 0; b < 65536; b++)
-      if (h[b]) has[lut[b]] = 1;
-    for (int g = 0; g < kGroups; g++) groups_used += has[g];
-  }
-  for (int b = 0; b < 512; b++) {
-    bool any = false;
-    for (int j = 0; j < 128 && !any; j++) any = h[b * 128 + j] != 0;
-    buckets_used += any;
-  }
-  if (groups_used < 2 * buckets_used) return SRS_OK;
-  for (int g = 0; g < kGroups; g++) {
-    const int diff = first[g] < 0 ? 0xFFFF : (first[g] ^ last[g]);
-    int bl = 0;
-    while ((1 << bl) <= diff) bl++;
-    rbits[g] = d.key_bits - (16 - bl);  // the group's keys share 16 - bl top bits
-  }
-  // Split table (DigitLut mode 3), where it balances about as well: each
-  // top-9-bit bin t gets 2^lg_t consecutive groups, the next lg_t key bits
-  // (uniform floats: one exponent's mantissas; no group spans two bins, so a
-  // group's keys are uniform below its prefix and the next level's digit
-  // splits them evenly). One 2 KB table and one lookup per key instead of the
-  // two-level 16-bit table (up to 24 KB staged per tile, two dependent lookups).
-  {
-    const int kb = d.key_bits;
-    std::vector<uint64_t> ct(512, 0), cnt1(kGroups, 0);
-    for (int t = 0; t < 512; t++)
-      for (int j = 0; j < 128; j++) ct[t] += h[t * 128 + j];
-    for (int b = 0; b < 65536; b++) cnt1[lut[b]] += h[b];
-    const uint64_t max1 = *std::max_element(cnt1.begin(), cnt1.end());
-    // bins worth less than one group share groups (consecutive, until their
-    // keys add up to one group's share): the tails of a float distribution
-    // would otherwise take a group per exponent
-    std::vector<int> lg(512, -1);     // own groups 2^lg; -1: none
-    std::vector<int> share(512, -1);  // >= 0: index of the shared group it joins
-    std::vector<uint64_t> shared_cnt;
-    int S = 0;
-    {
-      double acc = 0;
-      bool open = false;
-      for (int t = 0; t < 512; t++) {
-        if (!ct[t]) continue;
-        const double x = 512.0 * (double)ct[t] / (double)total;
-        if (x < 1.0) {
-          if (!open) {
-            shared_cnt.push_back(0);
-            S++;
-            open = true;
-            acc = 0;
-          }
-          share[t] = (int)shared_cnt.size() - 1;
-          shared_cnt.back() += ct[t];
-          acc += x;
-          if (acc >= 1.0) open = false;
-          continue;
-        }
-        open = false;
-        int l = 0;
-        while (l < 9 && (double)(2 << l) <= x) l++;
-        lg[t] = l;
-        S += 1 << l;
-      }
-    }
-    auto gsize = [&](int t, int l) { return (double)ct[t] / (double)(1 << l); };
-    while (S > 512) {  // over budget: halve where the resulting groups stay smallest
-      int best = -1;
-      for (int t = 0; t < 512; t++)
-        if (lg[t] > 0 && (best < 0 || gsize(t, lg[t] - 1) < gsize(best, lg[best] - 1))) best = t;
-      if (best < 0) break;
-      S -= 1 << (lg[best] - 1);
-      lg[best]--;
-    }
-    while (true) {  // spare budget: split the largest groups further
-      int best = -1;
-      for (int t = 0; t < 512; t++)
-        if (lg[t] >= 0 && lg[t] < 9 && (best < 0 || gsize(t, lg[t]) > gsize(best, lg[best])))
-          best = t;
-      if (best < 0 || S + (1 << lg[best]) > 512) break;
-      S += 1 << lg[best];
-      lg[best]++;
-    }
-    // predicted largest group (exact from the 16-bit bins while lg <= 7)
-    uint64_t max3 = 0;
-    for (uint64_t c : shared_cnt) max3 = std::max(max3, c);
-    for (int t = 0; t < 512; t++) {
-      if (lg[t] < 0) continue;
-      if (lg[t] <= 7) {
-        const int per = 128 >> lg[t];
-        for (int g = 0; g < (1 << lg[t]); g++) {
-          uint64_t c = 0;
-          for (int j = 0; j < per; j++) c += h[t * 128 + g * per + j];
-          max3 = std::max(max3, c);
-        }
-      } else {
-        max3 = std::max(max3, (ct[t] + (1u << lg[t]) - 1) >> lg[t]);
-      }
-    }
-    if (S <= 512 && max3 * 4 <= max1 * 5) {
-      // entry t: first group (bits 0..15) | lg (16..23); an empty bin joins
-      // the group before it (or the first group)
-      std::vector<int32_t> tab(512);
-      std::vector<uint64_t> glo(kGroups, ~0ull), ghi(kGroups, 0);
-      const int unit = kb - 9;  // key bits below the top 9
-      int run = 0, cur_share = -1;
-      for (int t = 0; t < 512; t++) {
-        const uint64_t t0 = (uint64_t)t << unit;
-        const uint64_t tl = t0 + ((uint64_t(1) << unit) - 1);
-        if (lg[t] < 0) {  // a shared group (a new one when its index changes), or an
-          int g;          // empty bin joining the group before it
-          if (share[t] >= 0 && share[t] != cur_share) {
-            cur_share = share[t];
-            g = run++;
-          } else {
-            g = run > 0 ? run - 1 : 0;
-          }
-          tab[t] = g;
-          glo[g] = std::min(glo[g], t0);
-          ghi[g] = std::max(ghi[g], tl);
-          continue;
-        }
-        tab[t] = run | (lg[t] << 16);
-        const int sub = unit - lg[t];
-        for (int j = 0; j < (1 << lg[t]); j++) {
-          const uint64_t a = t0 + ((uint64_t)j << sub);
-          glo[run + j] = std::min(glo[run + j], a);
-          ghi[run + j] = std::max(ghi[run + j], a + ((uint64_t(1) << sub) - 1));
-        }
-        run += 1 << lg[t];
-      }
-      for (int g = 0; g < kGroups; g++) {
-        if (glo[g] > ghi[g]) {
-          rbits[g] = kb;  // (no keys)
-          continue;
-        }
-        const uint64_t x = glo[g] ^ ghi[g];
-        rbits[g] = x ? 64 - __builtin_clzll(x) : 0;
-      }
-      SRS_TRY(ensure(W->lut, 512 * sizeof(int32_t)));
-      SRS_TRY(ensure(W->lut_rbits, kGroups * sizeof(int32_t)));
-      HIP_TRY(hipMemcpyAsync(W->lut.p, tab.data(), 512 * 4, hipMemcpyHostToDevice, st));
-      HIP_TRY(hipMemcpyAsync(W->lut_rbits.p, rbits.data(), rbits.size() * 4,
-                             hipMemcpyHostToDevice, st));
-      HIP_TRY(hipStreamSynchronize(st));  // the host vectors go out of scope
-      *lut_entries = 1024;  // (u16 units)
-      *lut_mode = 3;
-      *use = true;
-      if (trace_levels())
-        fprintf(stderr, "[srs] split table: %d groups, largest %llu vs %llu (16-bit table)\n", S,
-                (unsigned long long)max3, (unsigned long long)max1);
-      return SRS_OK;
-    }
-  }
+  const std::vector<int32_t>& lut = P.lut16;
   // two-level u16 table (DigitLut mode 1): a 12-bit bin whose 16 sub-bins
   // fall into one group maps straight to it; a split bin points to 16 entries
   std::vector<uint16_t> t2(4096);
@@ -2393,6 +2540,24 @@ int srs_debug_last_fallbacks(int64_t* counts) {
   HIP_TRY(hipMemcpy(&c, W->ctr.p, sizeof c, hipMemcpyDeviceToHost));
   counts[0] = (int64_t)(c.n_fallback + c.n_fallback1);
   counts[1] = (int64_t)c.n_fallback2;
+  return SRS_OK;
+}
+
+int srs_debug_plan_table(const uint32_t* hist, int64_t num, int key_bits, int32_t* mode,
+                         int32_t* groups, double* overflow, double* overflow_other,
+                         int32_t* table, int32_t* rbits) {
+  if (!hist || !mode || !table || !rbits || (key_bits != 32 && key_bits != 64) || num < 1)
+    return fail(SRS_ERR_INVALID_ARG, "srs_debug_plan_table: arguments");
+  std::vector<uint32_t> h(hist, hist + 65536);
+  TablePlan P;
+  plan_table(h, num, key_bits, &P);
+  *mode = P.mode;
+  if (groups) *groups = P.groups;
+  if (overflow) *overflow = P.over;
+  if (overflow_other) *overflow_other = P.over_other;
+  if (P.mode == 1) memcpy(table, P.lut16.data(), 65536 * 4);
+  if (P.mode == 3) memcpy(table, P.tab3.data(), 512 * 4);
+  if (P.mode) memcpy(rbits, P.rbits.data(), kGroups * 4);
   return SRS_OK;
 }
 

@@ -1,0 +1,119 @@
+"""CPU tests of the balanced first level's digit-table planner
+(srs_debug_plan_table: the host half of the sort's skewed-key level, no GPU).
+
+The planner turns the sampled 16-bit histogram of the transformed keys into
+512 key-range groups, either as a 16-bit bin -> group table (mode 1) or as a
+split table (mode 3: per top-9-bit bin, a first group and 2^lg groups by the
+next key bits). These tests rebuild the sort's own sample of C2's keys
+(BASELINE configs[2]: 1e9 float32 in [-1, 1), the bench generator), run the
+planner, and check what the sort relies on: group ids never decrease with the
+key, every group's keys share the bits above its rbits, the predicted
+next-level overflow is small, and the digit the GPU computes from the table
+(pass_digit, emulated here) agrees with the 16-bit view.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+
+srs_amd = pytest.importorskip("srs_amd")
+
+
+def _sm(x):
+    x = x + np.uint64(0x9E3779B97F4A7C15)
+    x = (x ^ (x >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+    x = (x ^ (x >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return x ^ (x >> np.uint64(31))
+
+
+def _c2_sample(n=10 ** 9, blocks=4096, chunk=1024):
+    """The transformed keys of the sort's sample of C2's input
+    (sample_hist16_kernel: `blocks` chunks of `chunk` keys, stride n / blocks)."""
+    stride = n // blocks
+    idx = (np.arange(blocks, dtype=np.uint64)[:, None] * np.uint64(stride) +
+           np.arange(chunk, dtype=np.uint64)[None, :]).ravel()
+    h = _sm(idx + np.uint64(42 << 32))
+    k = ((h >> np.uint64(40)).astype(np.int32).astype(np.float32) * np.float32(1.0 / 8388608.0) -
+         np.float32(1.0))
+    b = k.view(np.uint32)
+    return np.where(b >> np.uint32(31), ~b, b ^ np.uint32(1 << 31)).astype(np.uint32)
+
+
+def _plan(hist, n, key_bits):
+    L = srs_amd.lib()
+    f = L.srs_debug_plan_table
+    f.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.POINTER(ctypes.c_int32),
+                  ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_double),
+                  ctypes.POINTER(ctypes.c_double), ctypes.c_void_p, ctypes.c_void_p]
+    h = np.ascontiguousarray(hist, dtype=np.uint32)
+    table = np.zeros(65536, np.int32)
+    rbits = np.zeros(512, np.int32)
+    mode, groups = ctypes.c_int32(), ctypes.c_int32()
+    over, other = ctypes.c_double(), ctypes.c_double()
+    rc = f(h.ctypes.data, n, key_bits, ctypes.byref(mode), ctypes.byref(groups), ctypes.byref(over),
+           ctypes.byref(other), table.ctypes.data, rbits.ctypes.data)
+    assert rc == 0, L.srs_last_error()
+    return mode.value, groups.value, over.value, other.value, table, rbits
+
+
+def _digit(mode, table, u, key_bits):
+    """pass_digit of the table (srs_kernels.hip) on transformed keys u."""
+    u = u.astype(np.uint64)
+    if mode == 1:
+        return table[(u >> np.uint64(key_bits - 16)).astype(np.int64)]
+    e = table[:512][(u >> np.uint64(key_bits - 9)).astype(np.int64)].astype(np.int64)
+    lg = (e >> 16).astype(np.uint64)
+    sub = (u >> (np.uint64(key_bits - 9) - lg)) & ((np.uint64(1) << lg) - np.uint64(1))
+    return (e & 0xFFFF) + sub.astype(np.int64)
+
+
+def _check_groups(mode, table, rbits, u, key_bits):
+    d = _digit(mode, table, u, key_bits)
+    o = np.argsort(u, kind="stable")
+    assert np.all(np.diff(d[o]) >= 0), "group ids must not decrease with the key"
+    assert d.min() >= 0 and d.max() < 512
+    for g in np.unique(d):
+        ug = u[d == g].astype(np.uint64)
+        rb = int(rbits[g])
+        if rb < key_bits:
+            top = ug >> np.uint64(rb)
+            assert np.all(top == top[0]), f"group {g}: keys differ above bit {rb}"
+    return d
+
+
+def test_c2_plan_balances_the_next_level():
+    u = _c2_sample()
+    hist = np.bincount((u >> 16).astype(np.int64), minlength=65536)
+    mode, groups, over, other, table, rbits = _plan(hist, 10 ** 9, 32)
+    assert mode in (1, 3)
+    assert groups <= 512
+    # C2's round-3 grouping left 5 % of the keys (2101 buckets) above the LDS
+    # capacity after the second level; the plan must predict far less
+    assert over < 0.01 * 10 ** 9, (over, other)
+    d = _check_groups(mode, table, rbits, u, 32)
+    counts = np.bincount(d, minlength=512)
+    assert counts.max() <= 2.5 * len(u) / 512
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_skewed_u64_plan(seed):
+    """Exponentially skewed 64-bit keys (a few heavy top bins, a long tail)"""
+    rng = np.random.default_rng(seed)
+    u = (rng.exponential(2.0 ** 50, 1 << 22)).astype(np.uint64) + np.uint64(1 << 60)
+    hist = np.bincount((u >> np.uint64(48)).astype(np.int64), minlength=65536)
+    mode, groups, over, other, table, rbits = _plan(hist, 10 ** 9, 64)
+    assert mode in (0, 1, 3)
+    if mode:
+        _check_groups(mode, table, rbits, u, 64)
+
+
+def test_spread_keys_need_no_table():
+    """uniform 64-bit keys: every plain first digit is balanced; the planner
+    is not even asked (the sample says 'spread'), and if asked returns a
+    table whose groups still keep the key order"""
+    rng = np.random.default_rng(3)
+    u = rng.integers(0, 2 ** 63, 1 << 20, dtype=np.uint64) * np.uint64(2)
+    hist = np.bincount((u >> np.uint64(48)).astype(np.int64), minlength=65536)
+    mode, groups, over, other, table, rbits = _plan(hist, 10 ** 9, 64)
+    if mode:
+        _check_groups(mode, table, rbits, u, 64)
