@@ -448,7 +448,8 @@ def measure(cfg_name, args, torch, srs_amd, dist, dev, rank, world, shard):
     # from them). The same steps without the markers, for comparison:
     kstats = {}
     for name in ("count", "scatter", "local", "local_fast", "local_stable", "local_lsd", "scan",
-                 "plan", "children", "copy", "partition", "key_hist"):
+                 "plan", "children", "copy", "partition", "key_hist",
+                 *[f"{k}.L{i}" for i in range(1, 7) for k in ("count", "scatter")]):
         try:
             l, ms, el = srs_amd.kernel_stats(name)
         except Exception:

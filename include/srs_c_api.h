@@ -255,13 +255,20 @@ int srs_debug_last_local_counts(int64_t* counts);
 
 /* Placement diagnostics. srs_debug_alloc allocates `bytes` of
  * device memory on the current device the way mode says (0 = hipMalloc,
- * 1 = physically contiguous, 2 = hipMemCreate mapped at 1 GiB alignment; the
- * workspace's own big buffers follow SRS_WS_ALLOC = malloc|contig|vmm);
+ * 1 = physically contiguous, 2 = one hipMemCreate handle mapped at 1 GiB
+ * alignment, 3 / 4 = 2 MB handles mapped in a shuffled order / in order; the
+ * workspace's own big buffers follow SRS_WS_ALLOC = malloc|contig|vmm|
+ * vmmshuf|vmm2m);
  * srs_debug_free releases it. srs_debug_workspace reports the current
  * device's TMP and TMP2 buffers (NULL / 0 when not allocated). */
 int srs_debug_alloc(uint64_t bytes, int mode, void** ptr);
 int srs_debug_free(void* ptr);
 int srs_debug_workspace(void** tmp, uint64_t* tmp_bytes, void** tmp2, uint64_t* tmp2_bytes);
+/* Milliseconds of one pass of the scatter's write pattern (512 runs of 8
+ * elements per 4096-element tile into 16 MB windows) over [ptr, ptr + bytes)
+ * of device memory: the rate the sort's scatter and local passes can write
+ * that memory at. Synchronizes the device. */
+int srs_debug_probe_write(void* ptr, uint64_t bytes, float* ms);
 
 /* The balanced first level's digit table, planned on the host from a
  * 65536-bin histogram of the top 16 transformed key bits (the sample the

@@ -202,11 +202,19 @@ struct DevBuf {
 // SRS_WS_ALLOC selects how the big workspace buffers are backed (diagnostics
 // of the placement-dependent write rate): "malloc" (default,
 // hipMalloc), "contig" (hipExtMallocWithFlags(hipDeviceMallocContiguous):
-// one physically contiguous range) or "vmm" (hipMemCreate + hipMemMap into a
-// range reserved at 1 GiB alignment).
-enum BigAlloc { ALLOC_MALLOC = 0, ALLOC_CONTIG = 1, ALLOC_VMM = 2 };
+// one physically contiguous range), "vmm" (one hipMemCreate handle mapped
+// into a range reserved at 1 GiB alignment), "vmm2m" / "vmmshuf" (2 MB
+// handles mapped in order / in a shuffled order).
+enum BigAlloc {
+  ALLOC_MALLOC = 0,
+  ALLOC_CONTIG = 1,
+  ALLOC_VMM = 2,
+  ALLOC_VMM_SHUF = 3,
+  ALLOC_VMM_2M = 4,
+  ALLOC_MODES = 5
+};
 struct VmmRec {
-  hipMemGenericAllocationHandle_t h;
+  std::vector<hipMemGenericAllocationHandle_t> h;
   size_t size;
 };
 std::mutex g_vmu;
@@ -217,13 +225,17 @@ int ws_alloc_mode() {
   if (!e || !*e || !strcmp(e, "malloc")) return ALLOC_MALLOC;
   if (!strcmp(e, "contig")) return ALLOC_CONTIG;
   if (!strcmp(e, "vmm")) return ALLOC_VMM;
+  if (!strcmp(e, "vmmshuf")) return ALLOC_VMM_SHUF;
+  if (!strcmp(e, "vmm2m")) return ALLOC_VMM_2M;
   return ALLOC_MALLOC;
 }
+
+bool is_vmm(int mode) { return mode == ALLOC_VMM || mode == ALLOC_VMM_SHUF || mode == ALLOC_VMM_2M; }
 
 hipError_t big_alloc(void** p, size_t bytes, int mode) {
   *p = nullptr;
   if (mode == ALLOC_CONTIG) return hipExtMallocWithFlags(p, bytes, hipDeviceMallocContiguous);
-  if (mode != ALLOC_VMM) return hipMalloc(p, bytes);
+  if (!is_vmm(mode)) return hipMalloc(p, bytes);
   int dev = 0;
   hipError_t e = hipGetDevice(&dev);
   if (e != hipSuccess) return e;
@@ -235,49 +247,72 @@ hipError_t big_alloc(void** p, size_t bytes, int mode) {
   e = hipMemGetAllocationGranularity(&gran, &prop, hipMemAllocationGranularityRecommended);
   if (e != hipSuccess) return e;
   if (gran == 0) gran = size_t(2) << 20;
-  const size_t sz = (bytes + gran - 1) / gran * gran;
+  const size_t chunk_min = std::max<size_t>(gran, size_t(2) << 20);
+  size_t sz = (bytes + gran - 1) / gran * gran;
+  const size_t chunk = mode == ALLOC_VMM ? sz : chunk_min;
+  sz = (sz + chunk - 1) / chunk * chunk;
+  const size_t nch = sz / chunk;
   void* va = nullptr;
   e = hipMemAddressReserve(&va, sz, size_t(1) << 30, nullptr, 0);
   if (e != hipSuccess) return e;
-  hipMemGenericAllocationHandle_t h;
-  e = hipMemCreate(&h, sz, &prop, 0);
-  if (e != hipSuccess) {
-    (void)hipMemAddressFree(va, sz);
-    return e;
+  std::vector<size_t> slot(nch);
+  for (size_t k = 0; k < nch; k++) slot[k] = k;
+  if (mode == ALLOC_VMM_SHUF) {  // (a fixed permutation: reproducible placement)
+    uint64_t x = 0x9E3779B97F4A7C15ull;
+    for (size_t k = nch; k > 1; k--) {
+      x ^= x << 13;
+      x ^= x >> 7;
+      x ^= x << 17;
+      std::swap(slot[k - 1], slot[x % k]);
+    }
   }
-  e = hipMemMap(va, sz, 0, h, 0);
+  VmmRec rec;
+  rec.size = sz;
+  for (size_t k = 0; k < nch && e == hipSuccess; k++) {
+    hipMemGenericAllocationHandle_t h;
+    e = hipMemCreate(&h, chunk, &prop, 0);
+    if (e != hipSuccess) break;
+    rec.h.push_back(h);
+    e = hipMemMap((char*)va + slot[k] * chunk, chunk, 0, h, 0);
+  }
   if (e == hipSuccess) {
     hipMemAccessDesc a = {};
     a.location = prop.location;
     a.flags = hipMemAccessFlagsProtReadWrite;
     e = hipMemSetAccess(va, sz, &a, 1);
-    if (e != hipSuccess) (void)hipMemUnmap(va, sz);
   }
   if (e != hipSuccess) {
-    (void)hipMemRelease(h);
+    for (size_t k = 0; k < rec.h.size(); k++) {
+      (void)hipMemUnmap((char*)va + slot[k] * chunk, chunk);
+      (void)hipMemRelease(rec.h[k]);
+    }
     (void)hipMemAddressFree(va, sz);
     return e;
   }
   std::lock_guard<std::mutex> g(g_vmu);
-  g_vmm[va] = VmmRec{h, sz};
+  g_vmm[va] = std::move(rec);
   *p = va;
   return hipSuccess;
 }
 
 hipError_t big_free(void* p, int mode) {
   if (!p) return hipSuccess;
-  if (mode != ALLOC_VMM) return hipFree(p);
+  if (!is_vmm(mode)) return hipFree(p);
   VmmRec r;
   {
     std::lock_guard<std::mutex> g(g_vmu);
     auto it = g_vmm.find(p);
     if (it == g_vmm.end()) return hipErrorInvalidValue;
-    r = it->second;
+    r = std::move(it->second);
     g_vmm.erase(it);
   }
   (void)hipDeviceSynchronize();  // (unmapping does not wait for queued kernels)
   hipError_t e = hipMemUnmap(p, r.size);
-  hipError_t e2 = hipMemRelease(r.h);
+  hipError_t e2 = hipSuccess;
+  for (auto& h : r.h) {
+    const hipError_t x = hipMemRelease(h);
+    if (x != hipSuccess) e2 = x;
+  }
   hipError_t e3 = hipMemAddressFree(p, r.size);
   return e != hipSuccess ? e : e2 != hipSuccess ? e2 : e3;
 }
@@ -2565,8 +2600,8 @@ std::mutex g_dbg_amu;
 std::map<void*, int> g_dbg_allocs;  // srs_debug_alloc: pointer -> mode
 
 int srs_debug_alloc(uint64_t bytes, int mode, void** ptr) {
-  if (!ptr || mode < ALLOC_MALLOC || mode > ALLOC_VMM || bytes == 0)
-    return fail(SRS_ERR_INVALID_ARG, "srs_debug_alloc: ptr, mode 0..2 and bytes > 0");
+  if (!ptr || mode < ALLOC_MALLOC || mode >= ALLOC_MODES || bytes == 0)
+    return fail(SRS_ERR_INVALID_ARG, "srs_debug_alloc: ptr, mode 0..4 and bytes > 0");
   HIP_TRY(big_alloc(ptr, (size_t)bytes, mode));
   std::lock_guard<std::mutex> g(g_dbg_amu);
   g_dbg_allocs[*ptr] = mode;
@@ -2583,6 +2618,13 @@ int srs_debug_free(void* ptr) {
     g_dbg_allocs.erase(it);
   }
   HIP_TRY(big_free(ptr, mode));
+  return SRS_OK;
+}
+
+int srs_debug_probe_write(void* ptr, uint64_t bytes, float* ms) {
+  if (!ptr || !ms) return fail(SRS_ERR_INVALID_ARG, "srs_debug_probe_write: ptr and ms");
+  *ms = probe_write_ms(ptr, (size_t)bytes);
+  HIP_TRY(hipGetLastError());
   return SRS_OK;
 }
 

@@ -3462,6 +3462,60 @@ void launch_small_sort(int key_size, const SortDesc& d, Seg g, int64_t* taken, h
 #undef CALL
 }
 
+// ---------------------------------------------------------------------------
+// placement probe: the scatter's write pattern over a whole buffer
+// ---------------------------------------------------------------------------
+// A tile (256 threads) writes 4096 8-byte elements as 512 runs of 8 into 512
+// buckets of a 16 MB window: bucket r of window w starts at a hashed
+// 8-byte-aligned offset near r * 32 KB (as a C1 level's children do), tile i
+// of the window fills the i-th run of every bucket; windows in order, tiles
+// XCD-contiguous (xcd_remap). How fast this runs over a buffer says how fast
+// the scatter and local passes will write it.
+constexpr int64_t kProbeWindow = int64_t(16) << 20;
+__global__ __launch_bounds__(256) void place_probe_kernel(char* __restrict__ buf, int64_t windows) {
+  constexpr int kRuns = 512, kRunKeys = 8;
+  constexpr int64_t kSpan = kProbeWindow / kRuns;      // 32 KB per bucket
+  constexpr int64_t kTiles = kSpan / (kRunKeys * 8) / 2; // tiles per window (half of the span)
+  const int64_t t = xcd_remap(blockIdx.x, gridDim.x);
+  const int64_t w = t / kTiles, i = t % kTiles;
+  if (w >= windows) return;
+  const uint64_t v = (uint64_t)t * 0x9E3779B97F4A7C15ull;
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    const int e = k * 256 + (int)threadIdx.x;  // element of the tile
+    const int r = e >> 3, o = e & 7;
+    // bucket start: r * span + hash(r) * 8 inside the unused half of the span
+    const uint32_t hsh = (uint32_t)r * 2654435761u;
+    const int64_t start = r * kSpan + (int64_t)((hsh >> 20) % (uint32_t)(kSpan / 16)) * 8;
+    uint64_t* dst = (uint64_t*)(buf + w * kProbeWindow + start) + i * kRunKeys + o;
+    *dst = v + (uint64_t)e;
+  }
+}
+
+// Average milliseconds of one probe pass over [buf, buf + bytes) (2 passes
+// after one warmup; synchronous).
+float probe_write_ms(void* buf, size_t bytes) {
+  const int64_t windows = (int64_t)(bytes / kProbeWindow);
+  if (windows < 1) return 0.f;
+  constexpr int64_t kTiles = kProbeWindow / 512 / 64 / 2;
+  const unsigned grid = (unsigned)(windows * kTiles);
+  hipEvent_t a, b;
+  if (hipEventCreate(&a) != hipSuccess) return 0.f;
+  if (hipEventCreate(&b) != hipSuccess) {
+    (void)hipEventDestroy(a);
+    return 0.f;
+  }
+  place_probe_kernel<<<grid, 256>>>((char*)buf, windows);
+  (void)hipEventRecord(a, 0);
+  for (int k = 0; k < 2; k++) place_probe_kernel<<<grid, 256>>>((char*)buf, windows);
+  (void)hipEventRecord(b, 0);
+  float ms = 0.f;
+  if (hipEventSynchronize(b) != hipSuccess || hipEventElapsedTime(&ms, a, b) != hipSuccess) ms = 0.f;
+  (void)hipEventDestroy(a);
+  (void)hipEventDestroy(b);
+  return ms / 2;
+}
+
 void launch_fill(int64_t n, int kind, uint64_t seed, uint64_t first, void* keys,
                  int npay, const Col* pays, hipStream_t st) {
   fill_kernel<<<(unsigned)((n + 255) / 256), 256, 0, st>>>(n, kind, seed, first,

@@ -90,6 +90,7 @@ def lib() -> ctypes.CDLL:
                                    ctypes.POINTER(ctypes.c_double)]
     L.srs_debug_alloc.argtypes = [ctypes.c_uint64, ctypes.c_int, ctypes.POINTER(vp)]
     L.srs_debug_free.argtypes = [vp]
+    L.srs_debug_probe_write.argtypes = [vp, ctypes.c_uint64, ctypes.POINTER(ctypes.c_float)]
     L.srs_debug_workspace.argtypes = [ctypes.POINTER(vp), ctypes.POINTER(ctypes.c_uint64),
                                       ctypes.POINTER(vp), ctypes.POINTER(ctypes.c_uint64)]
     _lib = L
@@ -396,6 +397,13 @@ def debug_alloc(nbytes: int, mode: int = 0) -> int:
 
 def debug_free(ptr: int) -> None:
     _check(lib().srs_debug_free(ctypes.c_void_p(ptr)))
+
+
+def debug_probe_write(ptr: int, nbytes: int) -> float:
+    """ms of one pass of the scatter's write pattern over device memory."""
+    ms = ctypes.c_float()
+    _check(lib().srs_debug_probe_write(ctypes.c_void_p(ptr), int(nbytes), ctypes.byref(ms)))
+    return float(ms.value)
 
 
 def debug_workspace():

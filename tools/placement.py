@@ -141,7 +141,9 @@ def main():
         r = measure(L, n, keys.data_ptr(), pays.data_ptr(), ko, po, args.steps, stream)
         tmp = srs_amd.debug_workspace()
         print(json.dumps(dict(base, what="out", out=name, kout=hex(ko), pout=hex(po),
-                              tmp=hex(tmp[0]), fill_gbs=fill_rate(L, n, ko, po, stream), **r)),
+                              tmp=hex(tmp[0]), fill_gbs=fill_rate(L, n, ko, po, stream),
+                              probe_k=srs_amd.debug_probe_write(ko, 8 * n),
+                              probe_p=srs_amd.debug_probe_write(po, 8 * n), **r)),
               flush=True)
     # workspace placements, with the first output fixed
     name, ko, po, _ = outs[0]
@@ -150,7 +152,10 @@ def main():
         os.environ["SRS_WS_ALLOC"] = wm
         r = measure(L, n, keys.data_ptr(), pays.data_ptr(), ko, po, args.steps, stream)
         tmp = srs_amd.debug_workspace()
-        print(json.dumps(dict(base, what="ws", ws=wm, out=name, tmp=hex(tmp[0]), **r)), flush=True)
+        print(json.dumps(dict(base, what="ws", ws=wm, out=name, tmp=hex(tmp[0]),
+                              probe_t0=srs_amd.debug_probe_write(tmp[0], 8 * n),
+                              probe_t1=srs_amd.debug_probe_write(tmp[0] + 8 * n, 8 * n), **r)),
+              flush=True)
     # the first configuration again (drift check)
     srs_amd.release_workspace()
     os.environ["SRS_WS_ALLOC"] = "malloc"
