@@ -63,6 +63,9 @@ def parse():
     ap.add_argument("--extra", default="c2,c3",
                     help="comma list of further configs measured after the headline one and "
                          "reported under 'extra' (world 1, c1 headline only; 'none' = skip)")
+    ap.add_argument("--out-alloc", default="srs", choices=("srs", "torch"),
+                    help="memory of the out-of-place outputs: srs_alloc_device (placement "
+                         "probed, DESIGN.md §4) or torch's allocator")
     ap.add_argument("--dry-run-launch", action="store_true",
                     help="with --gpus N > 1 and no WORLD_SIZE: print the launcher's argv and "
                          "env as JSON instead of starting the ranks")
@@ -395,15 +398,22 @@ def measure(cfg_name, args, torch, srs_amd, dist, dev, rank, world, shard):
         make_dist_keys(keys, pays, args.dist, torch, srs_amd, kind)
     rec = rec_out = None
     keys_out, pays_out = None, []
+    def out_like(t):
+        """an output array like t: srs_alloc_device memory (the sort's writes
+        run at the rate of the placement it probes for) or torch's"""
+        if args.out_alloc == "torch":
+            return torch.empty_like(t)
+        return srs_amd.empty_device(t.numel(), t.dtype, t.device).view(t.shape)
+
     if layout == "aos":
         rec = torch.stack([keys, pays[0]], dim=1).contiguous()
-        rec_out = torch.empty_like(rec)
+        rec_out = out_like(rec)
         del keys, pays
         keys, pays = None, []
         rec_bytes = 16
     else:
-        keys_out = torch.empty_like(keys)
-        pays_out = [torch.empty_like(p) for p in pays]
+        keys_out = out_like(keys)
+        pays_out = [out_like(p) for p in pays]
         rec_bytes = keys.element_size() + sum(psizes)
     torch.cuda.synchronize()
 

@@ -201,6 +201,20 @@ int srs_partition_device(int64_t num, int key_kind, int up, const void* keys,
  * reference sorts on one host thread and has no counterpart. */
 int srs_set_host_devices(int32_t num_devices, const int32_t* devices);
 
+/* ---- device memory for sort buffers --------------------------------------- */
+
+/* Allocates `bytes` of device memory on the current device for arrays the
+ * sort will write (out-of-place outputs, in-place arrays). The scatter's
+ * write rate depends on where a buffer sits in HBM (the same
+ * kernel writes some allocations ~13 % slower); buffers of 256 MB and more
+ * are probed with the sort's write pattern and re-placed (up to 4 tries,
+ * while free memory allows) when slower than the fastest placement seen.
+ * The sort's own workspace is placed the same way. SRS_PLACE=0 turns the
+ * probing off. srs_free_device releases it. No counterpart in the
+ * reference (host arrays only). */
+int srs_alloc_device(uint64_t bytes, void** ptr);
+int srs_free_device(void* ptr);
+
 /* ---- synthetic data (bench / tests) ------------------------------------- */
 
 /* keys[i] = splitmix64(seed + first_index + i) truncated/reinterpreted to the

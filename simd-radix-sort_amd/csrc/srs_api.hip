@@ -317,12 +317,73 @@ hipError_t big_free(void* p, int mode) {
   return e != hipSuccess ? e : e2 != hipSuccess ? e2 : e3;
 }
 
+// ---- placed allocation ------------------------------------------------------
+// The scatter's and the local pass's write rate depends on where in HBM the
+// written buffer sits: the same 8 GB column written by the same kernel takes
+// ~6.2 or ~7.0 ms per scatter launch depending on the allocation (a probe of
+// the write pattern over the buffer separates the two at ~1.5 vs ~2.1 ms per
+// 8 GB). placed_alloc allocates a buffer, probes it, and while
+// its probe is slower than 1.12x the fastest rate seen in this process takes
+// another allocation (up to kPlaceTries, while free memory allows; the
+// rejected ones are held until the choice is made, so that each try gets
+// other memory), keeping the fastest. Small buffers are not probed.
+constexpr size_t kPlaceMinBytes = size_t(256) << 20;
+constexpr int kPlaceTries = 4;
+std::mutex g_plmu;
+double g_place_ref = 0;  // fastest probe seen, ms per GB (0: none yet)
+
+bool placement_enabled() {
+  const char* e = getenv("SRS_PLACE");  // SRS_PLACE=0: plain allocations (A/B runs)
+  return !(e && *e == '0');
+}
+
+hipError_t placed_alloc(void** p, size_t bytes, int mode) {
+  if (bytes < kPlaceMinBytes || !placement_enabled()) return big_alloc(p, bytes, mode);
+  std::lock_guard<std::mutex> g(g_plmu);
+  hipError_t e = hipDeviceSynchronize();  // (the probe runs on the null stream)
+  if (e != hipSuccess) return e;
+  void* best = nullptr;
+  double best_rate = 0;
+  const double ref = g_place_ref;  // the fastest placement of earlier buffers
+  std::vector<void*> rejected;
+  for (int k = 0; k < kPlaceTries; k++) {
+    if (k > 0) {
+      size_t fr = 0, tot = 0;
+      if (hipMemGetInfo(&fr, &tot) != hipSuccess || fr < bytes + bytes / 8) break;
+    }
+    void* c = nullptr;
+    e = big_alloc(&c, bytes, mode);
+    if (e != hipSuccess) {
+      if (best) break;  // (keep what we have)
+      return e;
+    }
+    const float ms = probe_write_ms(c, bytes);
+    const double rate = ms > 0 ? ms / ((double)bytes / 1e9) : 0;  // ms per GB
+    if (rate > 0 && (g_place_ref == 0 || rate < g_place_ref)) g_place_ref = rate;
+    if (!best || (rate > 0 && rate < best_rate)) {
+      if (best) rejected.push_back(best);
+      best = c;
+      best_rate = rate;
+    } else {
+      rejected.push_back(c);
+    }
+    if (best_rate <= 0) break;  // (no probe possible: keep it)
+    if (ref > 0 ? best_rate <= 1.12 * ref
+                : k > 0 && best_rate <= 1.12 * g_place_ref)  // (first buffer: two looks)
+      break;
+  }
+  for (void* r : rejected) (void)big_free(r, mode);
+  (void)hipGetLastError();
+  *p = best;
+  return hipSuccess;
+}
+
 void free_buf(DevBuf& b) {
   if (b.p) (void)big_free(b.p, b.mode);
   b = DevBuf();
 }
 
-int ensure(DevBuf& b, size_t bytes, int mode = ALLOC_MALLOC) {
+int ensure(DevBuf& b, size_t bytes, int mode = ALLOC_MALLOC, bool placed = false) {
   if (b.bytes >= bytes && b.p) return SRS_OK;
   if (b.p) {
     HIP_TRY(big_free(b.p, b.mode));
@@ -330,7 +391,8 @@ int ensure(DevBuf& b, size_t bytes, int mode = ALLOC_MALLOC) {
     b.bytes = 0;
   }
   size_t want = std::max<size_t>(bytes, 256);
-  HIP_TRY(big_alloc(&b.p, want, mode));
+  if (placed) HIP_TRY(placed_alloc(&b.p, want, mode));
+  else HIP_TRY(big_alloc(&b.p, want, mode));
   b.bytes = want;
   b.mode = mode;
   return SRS_OK;
@@ -1363,11 +1425,11 @@ int run_sort(Workspace* W, const Request& R, hipStream_t st) {
       tmp_bytes += align_up((size_t)n * R.widths[c], 256);  // (a pair: 8n bytes at tmp_off[1])
     }
   }
-  SRS_TRY(ensure(W->tmp, tmp_bytes, ws_alloc_mode()));
+  SRS_TRY(ensure(W->tmp, tmp_bytes, ws_alloc_mode(), true));
   char* tmp = (char*)W->tmp.p;
   char* tmp2 = nullptr;
   if (aos_cols || pair_cols) {
-    SRS_TRY(ensure(W->tmp2, tmp_bytes, ws_alloc_mode()));
+    SRS_TRY(ensure(W->tmp2, tmp_bytes, ws_alloc_mode(), true));
     tmp2 = (char*)W->tmp2.p;
     d.tmp2 = 1;
   }
@@ -2593,6 +2655,32 @@ int srs_debug_plan_table(const uint32_t* hist, int64_t num, int key_bits, int32_
   if (P.mode == 1) memcpy(table, P.lut16.data(), 65536 * 4);
   if (P.mode == 3) memcpy(table, P.tab3.data(), 512 * 4);
   if (P.mode) memcpy(rbits, P.rbits.data(), kGroups * 4);
+  return SRS_OK;
+}
+
+std::mutex g_pub_amu;
+std::map<void*, size_t> g_pub_allocs;  // srs_alloc_device
+
+int srs_alloc_device(uint64_t bytes, void** ptr) {
+  if (!ptr) return fail(SRS_ERR_INVALID_ARG, "srs_alloc_device: ptr is NULL");
+  *ptr = nullptr;
+  if (bytes == 0) return SRS_OK;
+  HIP_TRY(placed_alloc(ptr, (size_t)bytes, ALLOC_MALLOC));
+  std::lock_guard<std::mutex> g(g_pub_amu);
+  g_pub_allocs[*ptr] = (size_t)bytes;
+  return SRS_OK;
+}
+
+int srs_free_device(void* ptr) {
+  if (!ptr) return SRS_OK;
+  {
+    std::lock_guard<std::mutex> g(g_pub_amu);
+    auto it = g_pub_allocs.find(ptr);
+    if (it == g_pub_allocs.end())
+      return fail(SRS_ERR_INVALID_ARG, "srs_free_device: not from srs_alloc_device");
+    g_pub_allocs.erase(it);
+  }
+  HIP_TRY(hipFree(ptr));
   return SRS_OK;
 }
 

@@ -90,6 +90,8 @@ def lib() -> ctypes.CDLL:
                                    ctypes.POINTER(ctypes.c_double)]
     L.srs_debug_alloc.argtypes = [ctypes.c_uint64, ctypes.c_int, ctypes.POINTER(vp)]
     L.srs_debug_free.argtypes = [vp]
+    L.srs_alloc_device.argtypes = [ctypes.c_uint64, ctypes.POINTER(vp)]
+    L.srs_free_device.argtypes = [vp]
     L.srs_debug_probe_write.argtypes = [vp, ctypes.c_uint64, ctypes.POINTER(ctypes.c_float)]
     L.srs_debug_workspace.argtypes = [ctypes.POINTER(vp), ctypes.POINTER(ctypes.c_uint64),
                                       ctypes.POINTER(vp), ctypes.POINTER(ctypes.c_uint64)]
@@ -385,6 +387,48 @@ def last_local_counts():
     c = (ctypes.c_int64 * 2)()
     _check(lib().srs_debug_last_local_counts(c))
     return int(c[0]), int(c[1])
+
+
+class _DeviceBlock:
+    """srs_alloc_device memory exposed through __cuda_array_interface__; freed
+    when the last tensor viewing it goes away."""
+
+    def __init__(self, n, dtype, device):
+        import torch
+        self.device = torch.device(device)
+        self.dtype = dtype
+        self.n = int(n)
+        nbytes = self.n * torch.empty(0, dtype=dtype).element_size()
+        p = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            _check(lib().srs_alloc_device(nbytes, ctypes.byref(p)))
+        self.ptr = int(p.value or 0)
+        typestr = {torch.int64: "<i8", torch.int32: "<i4", torch.float32: "<f4",
+                   torch.float64: "<f8", torch.int16: "<i2", torch.uint8: "|u1",
+                   torch.int8: "|i1"}[dtype]
+        self.__cuda_array_interface__ = {"shape": (self.n,), "typestr": typestr,
+                                         "data": (self.ptr, False), "version": 2,
+                                         "strides": None}
+
+    def __del__(self):
+        if getattr(self, "ptr", 0):
+            try:
+                lib().srs_free_device(ctypes.c_void_p(self.ptr))
+            except Exception:
+                pass
+            self.ptr = 0
+
+
+def empty_device(n: int, dtype, device="cuda"):
+    """A 1-D torch tensor of n elements in memory from srs_alloc_device
+    (probed placement): for arrays the sort writes."""
+    import torch
+    blk = _DeviceBlock(n, dtype, device)
+    t = torch.as_tensor(blk, device=blk.device)
+    if t.data_ptr() != blk.ptr:
+        raise SrsError("empty_device: torch copied the block instead of viewing it")
+    t._srs_block = blk  # (keeps the memory alive as long as the tensor)
+    return t
 
 
 def debug_alloc(nbytes: int, mode: int = 0) -> int:

@@ -934,3 +934,24 @@ def test_copy_list_long_and_many_short_segments():
     assert torch.equal(outs[0], ref_k)
     assert torch.equal(outs[1], ref_i)
     assert torch.equal(outs[2], (ref_i & 0xFFFF).to(torch.int16))
+
+
+def test_placed_device_memory():
+    """srs_alloc_device (empty_device): the tensor views the placed block,
+    sorts into it match a sort into torch memory, the probe answers."""
+    torch = _torch()
+    n = (1 << 22) + 77
+    keys = torch.empty(n, dtype=torch.int64, device="cuda")
+    pays = torch.empty(n, dtype=torch.int64, device="cuda")
+    srs_amd.fill_synthetic_device(keys, pays, seed=5 << 32, key_kind=srs_amd.KEY_U64)
+    ko, po = srs_amd.empty_device(n, torch.int64), srs_amd.empty_device(n, torch.int64)
+    assert ko.is_cuda and ko.numel() == n and ko.dtype == torch.int64
+    ko2, po2 = torch.empty_like(keys), torch.empty_like(pays)
+    srs_amd.sort_device(keys, pays, key_kind=srs_amd.KEY_U64, out=(ko, po))
+    srs_amd.sort_device(keys, pays, key_kind=srs_amd.KEY_U64, out=(ko2, po2))
+    torch.cuda.synchronize()
+    assert torch.equal(ko, ko2) and torch.equal(po, po2)
+    big = srs_amd.empty_device(1 << 28, torch.int64)  # 2 GB: probed placement
+    assert srs_amd.debug_probe_write(big.data_ptr(), 8 << 28) > 0
+    del big, ko, po
+    torch.cuda.synchronize()
