@@ -21,6 +21,7 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <queue>
 #include <string>
 #include <thread>
 #include <vector>
@@ -613,8 +614,18 @@ struct TablePlan {
 
 void plan_table(const std::vector<uint32_t>& h, int64_t n, int key_bits, TablePlan* P) {
   *P = TablePlan();
+  // (host time here is GPU idle time: every pass below looks only at the
+  // non-empty bins or is a plain integer sweep)
+  std::vector<uint64_t> ct(512, 0);
+  std::vector<int32_t> nz;  // the non-empty bins
+  nz.reserve(8192);
+  for (int b = 0; b < 65536; b++)
+    if (h[b]) {
+      nz.push_back(b);
+      ct[b >> 7] += h[b];
+    }
   uint64_t total = 0;
-  for (uint32_t v : h) total += v;
+  for (uint64_t c : ct) total += c;
   if (total == 0) return;
   // Bins -> groups. Candidate groupings of the 16-bit bins into 512 key-range
   // groups; the one whose next level is predicted to leave the fewest keys in
@@ -627,19 +638,25 @@ void plan_table(const std::vector<uint32_t>& h, int64_t n, int key_bits, TablePl
   //    own, cut at 16-bit bins by key counts; bins worth less share groups of
   //    at most one share.
   const double to_n = (double)n / (double)total;  // sample -> input keys
-  std::vector<uint64_t> ct(512, 0);
-  for (int t = 0; t < 512; t++)
-    for (int j = 0; j < 128; j++) ct[t] += h[t * 128 + j];
   // predicted keys the next level leaves in buckets above kLocalCap (keys
   // uniform inside a 16-bit bin), or that need two more levels
+  std::vector<double> qsum(kMaxBins, 0.0);
   auto overflow = [&](const std::vector<int32_t>& L) -> double {
-    std::vector<int32_t> fst(kGroups, -1), lst(kGroups, -1);
+    // a group's bins are one run of the (monotone) table
+    std::vector<int32_t> fst(kGroups, -1), lst(kGroups, -1), nz0(kGroups, 0), nz1(kGroups, 0);
     std::vector<uint64_t> cnt(kGroups, 0);
-    for (int b = 0; b < 65536; b++) {
-      const int g = L[b];
-      if (fst[g] < 0) fst[g] = b;
-      lst[g] = b;
-      cnt[g] += h[b];
+    fst[L[0]] = 0;
+    for (int b = 1; b < 65536; b++)
+      if (L[b] != L[b - 1]) {
+        lst[L[b - 1]] = b - 1;
+        fst[L[b]] = b;
+      }
+    lst[L[65535]] = 65535;
+    for (size_t i = 0; i < nz.size(); i++) {  // the group's non-empty bins: nz[nz0, nz1)
+      const int g = L[nz[i]];
+      if (!cnt[g]) nz0[g] = (int32_t)i;
+      nz1[g] = (int32_t)i + 1;
+      cnt[g] += h[nz[i]];
     }
     double over = 0;
     for (int g = 0; g < kGroups; g++) {
@@ -654,29 +671,39 @@ void plan_table(const std::vector<uint32_t>& h, int64_t n, int key_bits, TablePl
       }
       const int bits = choose_bits((int64_t)len, key_bits - (16 - bl));
       if (bits >= bl) {  // each bin splits into 2^(bits - bl) buckets
-        for (int b = fst[g]; b <= lst[g]; b++)
-          if ((double)h[b] * to_n / (double)(1 << (bits - bl)) > kLocalCap) over += h[b] * to_n;
+        const double lim = (double)kLocalCap * (double)(1 << (bits - bl)) / to_n;
+        for (int i = nz0[g]; i < nz1[g]; i++)
+          if ((double)h[nz[i]] > lim) over += h[nz[i]] * to_n;
       } else {  // each bucket spans 2^(bl - bits) bins of the aligned range
-        const int span = 1 << (bl - bits), b0 = fst[g] & ~((1 << bl) - 1);
-        for (int q = 0; q < (1 << bits); q++) {
-          double c = 0;
-          for (int b = std::max(fst[g], b0 + q * span); b < b0 + (q + 1) * span && b <= lst[g]; b++)
-            c += h[b];
-          if (c * to_n > kLocalCap) over += c * to_n;
+        const int sh = bl - bits, b0 = fst[g] & ~((1 << bl) - 1);
+        int qlo = kMaxBins, qhi = -1;
+        for (int i = nz0[g]; i < nz1[g]; i++) {
+          const int q = (nz[i] - b0) >> sh;
+          qsum[q] += h[nz[i]];
+          qlo = std::min(qlo, q);
+          qhi = std::max(qhi, q);
+        }
+        for (int q = qlo; q <= qhi; q++) {
+          if (qsum[q] * to_n > kLocalCap) over += qsum[q] * to_n;
+          qsum[q] = 0;
         }
       }
     }
     return over;
   };
   std::vector<int32_t> lut(65536), first(kGroups, -1), last(kGroups, -1), rbits(kGroups);
-  {
+  {  // (an empty bin takes the group before it)
     double before = 0;
-    for (int b = 0; b < 65536; b++) {
-      int g = (int)((before + 0.5 * h[b]) * kGroups / (double)total);
-      g = std::min(std::max(g, b ? lut[b - 1] : 0), kGroups - 1);
+    int g = 0, at = 0;
+    for (int b : nz) {
+      std::fill(lut.begin() + at, lut.begin() + b, g);
+      const int x = (int)((before + 0.5 * h[b]) * kGroups / (double)total);
+      g = std::min(std::max(x, g), kGroups - 1);
       lut[b] = g;
+      at = b + 1;
       before += h[b];
     }
+    std::fill(lut.begin() + at, lut.end(), g);
   }
   double over_best = overflow(lut);
   {
@@ -751,15 +778,10 @@ void plan_table(const std::vector<uint32_t>& h, int64_t n, int key_bits, TablePl
   int groups_used = 0, buckets_used = 0;
   {
     std::vector<uint8_t> has(kGroups, 0);
-    for (int b = 0; b < 65536; b++)
-      if (h[b]) has[lut[b]] = 1;
+    for (int b : nz) has[lut[b]] = 1;
     for (int g = 0; g < kGroups; g++) groups_used += has[g];
   }
-  for (int b = 0; b < 512; b++) {
-    bool any = false;
-    for (int j = 0; j < 128 && !any; j++) any = h[b * 128 + j] != 0;
-    buckets_used += any;
-  }
+  for (int t = 0; t < 512; t++) buckets_used += ct[t] != 0;
   if (groups_used < 2 * buckets_used) return;
   for (int g = 0; g < kGroups; g++) {
     const int diff = first[g] < 0 ? 0xFFFF : (first[g] ^ last[g]);
@@ -806,23 +828,32 @@ void plan_table(const std::vector<uint32_t>& h, int64_t n, int key_bits, TablePl
       }
     }
     auto gsize = [&](int t, int l) { return (double)ct[t] / (double)(1 << l); };
-    while (S > 512) {  // over budget: halve where the resulting groups stay smallest
-      int best = -1;
+    {  // over budget: halve where the resulting groups stay smallest (min-heap)
+      std::priority_queue<std::pair<double, int>, std::vector<std::pair<double, int>>,
+                          std::greater<std::pair<double, int>>> q;
       for (int t = 0; t < 512; t++)
-        if (lg[t] > 0 && (best < 0 || gsize(t, lg[t] - 1) < gsize(best, lg[best] - 1))) best = t;
-      if (best < 0) break;
-      S -= 1 << (lg[best] - 1);
-      lg[best]--;
+        if (lg[t] > 0) q.push({gsize(t, lg[t] - 1), t});
+      while (S > 512 && !q.empty()) {
+        const int t = q.top().second;
+        q.pop();
+        S -= 1 << (lg[t] - 1);
+        lg[t]--;
+        if (lg[t] > 0) q.push({gsize(t, lg[t] - 1), t});
+      }
     }
-    while (true) {  // spare budget: split the largest groups that still fit
-      int best = -1;
+    {  // spare budget: split the largest groups that still fit (max-heap; a
+       // bin whose doubling does not fit now never will: the budget only shrinks)
+      std::priority_queue<std::pair<double, int>> q;
       for (int t = 0; t < 512; t++)
-        if (lg[t] >= 0 && lg[t] < 9 && S + (1 << lg[t]) <= 512 &&
-            (best < 0 || gsize(t, lg[t]) > gsize(best, lg[best])))
-          best = t;
-      if (best < 0) break;
-      S += 1 << lg[best];
-      lg[best]++;
+        if (lg[t] >= 0 && lg[t] < 9) q.push({gsize(t, lg[t]), t});
+      while (!q.empty()) {
+        const int t = q.top().second;
+        q.pop();
+        if (S + (1 << lg[t]) > 512) continue;
+        S += 1 << lg[t];
+        lg[t]++;
+        if (lg[t] < 9) q.push({gsize(t, lg[t]), t});
+      }
     }
     // the same grouping at 16-bit resolution (representable while lg <= 7)
     bool repr = S <= 512;
@@ -850,7 +881,9 @@ void plan_table(const std::vector<uint32_t>& h, int64_t n, int key_bits, TablePl
       }
     }
     const double over3 = repr ? overflow(l3) : 1e300;
-    if (repr && over3 <= over_best) {
+    const char* force = getenv("SRS_TABLE");  // (A/B runs: "1" or "3" forces the table kind)
+    const bool take3 = force && *force ? (*force == '3' && repr) : (repr && over3 <= over_best);
+    if (take3) {
       // entry t: first group (bits 0..15) | lg (16..23); shared and empty
       // bins: the group (lg 0)
       std::vector<int32_t> tab(512);
