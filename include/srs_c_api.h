@@ -187,6 +187,44 @@ int srs_partition_device(int64_t num, int key_kind, int up, const void* keys,
                          void* keys_out, void* const* payloads_out,
                          int64_t* part_counts, void* stream);
 
+/* ---- the multi-GPU shard sort over RCCL (C ABI) ------------
+ * One array spread over N GPUs is sorted across them: rank r ends with the
+ * r-th key range, so concatenating the ranks' outputs gives the sorted array
+ * (stable). The protocol is the one above: histogram all-reduce, 512
+ * key-range groups, chunked partition, rounds of grouped send/recv over
+ * xGMI, each round's range sorted on a side stream while the next is in
+ * flight. RCCL is loaded at first use (librccl.so.1); without it these
+ * return SRS_ERR_NO_DEVICE. The reference has no multi-device path.
+ *
+ * Communicators: one process per GPU (srs_shard_unique_id on one rank, the
+ * 128 bytes passed to every rank, srs_shard_comm_init on each with its GPU
+ * current), or one process driving several GPUs (srs_shard_comm_init_all,
+ * then srs_shard_sort_multi). */
+#define SRS_SHARD_ID_BYTES 128
+typedef struct srs_shard_comm_s* srs_shard_comm;
+int srs_shard_unique_id(void* id);
+int srs_shard_comm_init(int32_t world, int32_t rank, const void* id, srs_shard_comm* comm);
+int srs_shard_comm_init_all(int32_t num_devices, const int32_t* devices, srs_shard_comm* comms);
+int srs_shard_comm_destroy(srs_shard_comm comm);
+
+/* This rank's part of the shard sort of device columns (inputs untouched):
+ * *keys_out / payloads_out[k] receive device pointers to this rank's sorted
+ * key range and *num_out its length; the memory belongs to the communicator
+ * and stays valid until its next sort or its destruction. On `stream`; every
+ * rank of the communicator must call it. */
+int srs_shard_sort_device(srs_shard_comm comm, int64_t num, int key_kind, int up,
+                          const void* keys, int32_t num_payloads, const void* const* payloads,
+                          const uint32_t* payload_sizes, void** keys_out, void** payloads_out,
+                          int64_t* num_out, void* stream);
+
+/* All ranks of a single-process communicator set at once (one host thread
+ * per GPU; synchronous): rank i sorts nums[i] records at keys[i] and
+ * payloads[i * num_payloads + k]; outputs as above, per rank. */
+int srs_shard_sort_multi(int32_t num_devices, const srs_shard_comm* comms, const int64_t* nums,
+                         int key_kind, int up, const void* const* keys, int32_t num_payloads,
+                         const void* const* payloads, const uint32_t* payload_sizes,
+                         void** keys_out, void** payloads_out, int64_t* nums_out);
+
 /* ---- host arrays over several GPUs --------------------------------------- */
 
 /* Devices the host-pointer entry points (srs_sort_soa, srs_sort_soa_leaf)

@@ -2377,6 +2377,9 @@ int set_leaf_mode(Request& R, int leaf_mode) {
 }
 
 }  // namespace
+
+// (other translation units of the library report errors through this)
+int set_error(int code, const std::string& msg) { return fail(code, msg); }
 }  // namespace srs
 
 using namespace srs;

@@ -137,7 +137,8 @@ def test_library_matches_the_sources():
     import srs_amd
     pkg = os.path.join(REPO, "simd-radix-sort_amd")
     files = [os.path.join(pkg, "csrc", f) for f in ("srs_kernels.hip", "srs_api.hip",
-                                                    "srs_common.h", "srs_kernels.h")]
+                                                    "srs_shard.hip", "srs_common.h",
+                                                    "srs_kernels.h")]
     files.append(HEADER)
     h = hashlib.sha256(b"".join(open(f, "rb").read() for f in files)).hexdigest()[:16]
     v = srs_amd.version()
