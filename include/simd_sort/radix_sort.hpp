@@ -73,7 +73,8 @@ struct CmpSorterInsertionSort {};
 // element ends within cmpSortThreshold of its sorted position (thesis
 // 3113-3124). On the GPU the local pass skips its in-bucket rank when every
 // bucket holds <= cmpSortThreshold keys (SRS_LEAF_UNSORTED); every leaf holds
-// exactly the elements a full sort puts there.
+// exactly the elements a full sort puts there. The order inside a leaf is
+// unspecified and may differ between runs.
 struct CmpSorterNoSort {};
 // src/cmp_sorters.hpp:40-63 (needs the vendored bramas sorters there): the
 // leaves are sorted (as here); the reference's type restrictions are kept

@@ -102,7 +102,10 @@ int srs_sort_aos(int64_t num, int key_kind, int up, int64_t cmp_sort_threshold,
  * leaves of <= cmp_sort_threshold keys and leaves them in partition order.
  * Every leaf then holds exactly the keys (and their payloads) a full sort
  * puts there, so each element ends within cmp_sort_threshold - 1 places of
- * its sorted slot; num <= cmp_sort_threshold leaves the input untouched. */
+ * its sorted slot; num <= cmp_sort_threshold leaves the input untouched.
+ * The order inside a leaf is unspecified and may differ from run to run (the
+ * GPU's bucket pass places a leaf's elements with LDS atomics); only the
+ * leaf's contents are guaranteed, as for the reference's no-op leaf. */
 #define SRS_LEAF_SORTED 0
 #define SRS_LEAF_UNSORTED 1
 
