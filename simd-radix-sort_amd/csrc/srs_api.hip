@@ -665,7 +665,7 @@ void plan_table(const std::vector<uint32_t>& h, int64_t n, int key_bits, TablePl
       int bl = 0;
       while ((1 << bl) <= (fst[g] ^ lst[g])) bl++;
       int need;
-      if (levels_for((int64_t)len, kLocalTarget, &need) > 1) {
+      if (levels_for((int64_t)len, kLocalCapTarget, &need) > 1) {
         over += len;
         continue;
       }
@@ -1060,8 +1060,10 @@ struct LevelMode {
   bool home = false;                // every bucket of this level is final: scatter to OUT
 };
 
+// lut: 0 a plain digit, 1 a digit table of any kind, 2 a small kind (key
+// ranges, split table: the kernels with the small LDS table)
 int run_level(Workspace* W, int ks, const SortDesc* d_desc, LevelState& S, int force_bits,
-              bool lut, hipStream_t st, const int32_t* lut_rbits = nullptr,
+              int lut, hipStream_t st, const int32_t* lut_rbits = nullptr,
               const LevelMode& M = LevelMode()) {
   const int64_t nbig = S.nbig;
   ListCounters* d_ctr = (ListCounters*)W->ctr.p;
@@ -1599,7 +1601,7 @@ int run_sort(Workspace* W, const Request& R, hipStream_t st) {
     m1.key_bits = d.key_bits;
     ++level;
     if (balanced)
-      SRS_TRY(run_level(W, ksl, d_desc, S, kMaxDigitBits, true, st,
+      SRS_TRY(run_level(W, ksl, d_desc, S, kMaxDigitBits, d.lut_mode >= 2 ? 2 : 1, st,
                         (const int32_t*)W->lut_rbits.p, m1));
     else
       SRS_TRY(run_level(W, ksl, d_desc, S, -b1, false, st, nullptr, m1));
@@ -1615,7 +1617,7 @@ int run_sort(Workspace* W, const Request& R, hipStream_t st) {
     ++level;
     LevelMode m0;
     m0.home = ranges_final;  // (single-valued buckets: written home directly)
-    SRS_TRY(run_level(W, ksl, d_desc, S, kMaxDigitBits, true, st,
+    SRS_TRY(run_level(W, ksl, d_desc, S, kMaxDigitBits, d.lut_mode >= 2 ? 2 : 1, st,
                       (const int32_t*)W->lut_rbits.p, m0));
   }
   while (S.nbig > 0) {
@@ -1758,7 +1760,7 @@ int run_partition(Workspace* W, const Request& R, int bits, const int32_t* d_lut
   int fb = 1;
   while ((1 << fb) < nparts) fb++;
   LevelState S{1, 0, 0, 0, 0, d.ncols, 0};
-  SRS_TRY(run_level(W, ks, d_desc, S, aligned ? -fb : fb, !aligned, st));
+  SRS_TRY(run_level(W, ks, d_desc, S, aligned ? -fb : fb, aligned ? 0 : 1, st));
   // group sizes from the segment's bucket bases (sbase row 0)
   std::vector<uint64_t> sb((size_t)1 << fb);
   HIP_TRY(hipMemcpyAsync(sb.data(), W->sbase.p, sb.size() * 8, hipMemcpyDeviceToHost, st));

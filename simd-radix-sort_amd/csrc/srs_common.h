@@ -258,12 +258,24 @@ __host__ __device__ inline int levels_for(int64_t len, int64_t target, int* need
   return (need + kMaxDigitBits - 1) / kMaxDigitBits;
 }
 
+// average bucket up to which a segment still takes one level fewer: its
+// buckets then land in the large LDS class (<= kLocalCap records, ~2.5x the
+// small class's cost per key) instead of paying a count + scatter level and
+// its launches and host sync (C2's few oversized first-level groups: a
+// third and fourth level on ~1 % of the keys)
+constexpr int kLocalCapTarget = 7680;
+
 __host__ __device__ inline int choose_bits(int64_t len, int rbits) {
   // bits needed to bring buckets under kLocalTarget, spread evenly over the
   // levels that takes (<= kMaxDigitBits each); one more bit when that lands
   // the buckets in the smaller (faster) LDS class without an extra level
-  int need, need_small;
-  const int levels = levels_for(len, kLocalTarget, &need);
+  int need, need_small, need_cap;
+  int levels = levels_for(len, kLocalTarget, &need);
+  const int levels_cap = levels_for(len, kLocalCapTarget, &need_cap);
+  if (levels_cap < levels) {
+    levels = levels_cap;
+    need = need_cap;
+  }
   const int levels_small = levels_for(len, kLocalSmallTarget, &need_small);
   if (levels_small == levels) need = need_small;
   int bits = (need + levels - 1) / levels;

@@ -25,7 +25,7 @@ void launch_plan_bases(SegPlan* plan, int64_t nbig, const int64_t* tbase,
                        const int64_t* gbase, hipStream_t st);
 void launch_count(int key_size, const SortDesc* d, const SegPlan* plan,
                   const int32_t* tile_seg, int64_t ntiles, uint16_t* hist,
-                  unsigned long long* var_or, bool lut, hipStream_t st,
+                  unsigned long long* var_or, int lut, hipStream_t st,
                   const GTile* gt = nullptr, const int32_t* torder = nullptr);
 int64_t scan_temp_elems(int64_t n);
 void launch_excl_scan(const uint64_t* x, uint64_t* y, int64_t n, uint64_t* temp,
@@ -38,7 +38,7 @@ void launch_offsets(SegPlan* plan, int64_t nbig, const int32_t* group_seg, int64
                     uint32_t* prun = nullptr);
 void launch_scatter(int key_size, const SortDesc* d, const SegPlan* plan,
                     const int32_t* tile_seg, const uint64_t* offs, const uint32_t* offs32,
-                    int64_t ntiles, bool lut, int ncols, hipStream_t st,
+                    int64_t ntiles, int lut, int ncols, hipStream_t st,
                     const GTile* gt = nullptr);
 // stripe first level -> the second level's segment list (W->big, n_big),
 // tile counts (nt_over) and gathered tile table (gt); see GTile

@@ -263,7 +263,7 @@ struct DigitLut {
 
 // Digit of a transformed key for a global pass: the key's bits
 // [shift, shift + bits), or (LUT) a group id looked up by its top bits.
-template <bool LUT, typename U>
+template <int LUT, typename U>
 __device__ __forceinline__ uint32_t pass_digit(U u, int shift, uint32_t mask, const DigitLut& L) {
   if constexpr (LUT) {
     if (L.mode == 2) {  // range c = #{k : u > hi_k} (unused ranges: hi = ~0)
@@ -654,13 +654,30 @@ __device__ __forceinline__ int64_t xcd_remap(int64_t bid, int64_t nwg) {
 // global lookup made the LUT scatter 1.7x slower than a plain digit pass.
 // Tables up to 2^kLdsLutBits entries are staged in LDS instead (the caller
 // barriers before the first use). Returns the table to read.
-template <bool LUT, int NT>
+// LDS the digit table of a pass takes (u16 entries): LUT 1 any table kind
+// (up to the 24 KB two-level table), LUT 2 the small kinds only (key ranges,
+// the 2 KB split table), 0 none. The small instantiations keep the count at
+// eight waves per SIMD and the scatter's staged digits.
+template <int LUT>
+constexpr int kLutLdsEntries = LUT == 1 ? kLdsLutEntries : LUT == 2 ? 1024 : 8;
+
+template <int LUT, int NT>
 __device__ __forceinline__ DigitLut stage_lut(const SortDesc* desc, uint16_t* slut) {
   DigitLut L{};
   if (!LUT) return L;
   L.shift = desc->lut_shift;
   L.mode = desc->lut_mode;
   L.r = desc;
+  if constexpr (LUT == 2) {  // (small kinds only: the host never sends others here)
+    if (L.mode == 3) {
+      typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+      const __amdgpu_buffer_rsrc_t r = strip_rsrc((const char*)desc->digit_lut, 2048u);
+      for (uint32_t i = threadIdx.x; i < 128u; i += NT)
+        ((u32x4*)slut)[i] = __builtin_amdgcn_raw_buffer_load_b128(r, i * 16u, 0, 0);
+      L.s = slut;
+    }
+    return L;
+  }
   if (L.mode == 2) {  // key ranges: no table to stage
   } else if (L.mode == 3) {  // split table: 512 u32 entries (2 KB)
     typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -810,7 +827,7 @@ __device__ __forceinline__ CountTile count_load(const SortDesc* __restrict__ des
 }
 
 // Counts a loaded tile into h (LDS, zeroed) and ORs its varying bits into *sor.
-template <typename KT, typename U, bool LUT, bool CZ>
+template <typename KT, typename U, int LUT, bool CZ>
 __device__ __forceinline__ void count_add(const SortDesc* __restrict__ desc,
                                           const SegPlan* __restrict__ plan, const CountTile& T,
                                           const U (&raw)[kCountItems], U uref_raw,
@@ -884,7 +901,7 @@ __device__ __forceinline__ void count_flush(const SegPlan* __restrict__ plan, co
   }
 }
 
-template <typename KT, typename U, bool LUT, bool CZ>
+template <typename KT, typename U, int LUT, bool CZ>
 __global__ __launch_bounds__(kCountThreads) void count_kernel(
     const SortDesc* __restrict__ desc, const SegPlan* __restrict__ plan,
     const int32_t* __restrict__ tile_seg, uint16_t* __restrict__ hist,
@@ -897,7 +914,7 @@ __global__ __launch_bounds__(kCountThreads) void count_kernel(
   // gathered level: tiles in stripe order (each stripe's pieces lie back to
   // back, so the reads sweep memory); the rows do not depend on the order
   if (torder && kCountTiles == 1) t0 = torder[t0];
-  __shared__ alignas(16) uint16_t slut[LUT ? kLdsLutEntries : 8];
+  __shared__ alignas(16) uint16_t slut[kLutLdsEntries<LUT>];
   U ra[kCountItems], rb[kCountItems];
   U ua, ub;
   CountTile A = count_load<KT, U>(desc, plan, tile_seg, gt, t0, ntiles, ra, ua);
@@ -1315,12 +1332,12 @@ __global__ void stripe_gtile_kernel(const uint32_t* __restrict__ prun,
 // waited for (LDS-only barriers between columns). One tile per workgroup,
 // two 16-wave workgroups per CU (<= 64 VGPRs); persistent variants that
 // prefetch the next tile measured slower.
-template <bool LUT>
+template <int LUT>
 struct ScatterLds {
   uint64_t sval[kTile];
   // digit of each staged slot (LUT passes recompute it instead: their 24 KB
   // table must leave room for two workgroups per CU)
-  uint16_t sdig[(LUT || !SRS_SCATTER_SDIG) ? 1 : kTile];
+  uint16_t sdig[(LUT == 1 || !SRS_SCATTER_SDIG) ? 1 : kTile];
   alignas(8) uint16_t wc[kScatterThreads / 64][kMaxBins];  // zeroed as u64
   uint16_t bin_start[kMaxBins];  // tile offsets <= kTile fit 16 bits
   int64_t gdst[kMaxBins];
@@ -1425,7 +1442,7 @@ __device__ __forceinline__ TileInfo scatter_load_tile(
   return ti;
 }
 
-template <typename KT, typename U, bool LUT, bool CZ, bool PRE3>
+template <typename KT, typename U, int LUT, bool CZ, bool PRE3>
 __device__ __forceinline__ void scatter_process_tile(
     const SortDesc* __restrict__ desc, const SegPlan* __restrict__ plan, ScatterLds<LUT>& L,
     const TileInfo& ti, int ncols, const uint64_t (&v0)[kScatterItems],
@@ -1534,7 +1551,7 @@ __device__ __forceinline__ void scatter_process_tile(
         if (j < cnt) {
           const uint64_t x = L.sval[j];
           uint32_t d;
-          if constexpr (LUT || !SRS_SCATTER_SDIG) d = pass_digit<LUT>(xf((U)(x & kmask)), P.shift, mask, lut);
+          if constexpr (LUT == 1 || !SRS_SCATTER_SDIG) d = pass_digit<LUT>(xf((U)(x & kmask)), P.shift, mask, lut);
           else d = L.sdig[j];
           dout[i] = (uint16_t)d;
           #ifdef SRS_DIAG_SEQW
@@ -1622,13 +1639,13 @@ __device__ __forceinline__ void scatter_process_tile(
 }
 
 // One tile per workgroup (XCD-aware order).
-template <typename KT, typename U, bool LUT, bool CZ, bool PRE3>
+template <typename KT, typename U, int LUT, bool CZ, bool PRE3>
 __global__ __launch_bounds__(kScatterThreads, SRS_SCATTER_WAVES_PER_EU) void scatter_kernel(
     const SortDesc* __restrict__ desc, const SegPlan* __restrict__ plan,
     const int32_t* __restrict__ tile_seg, const uint64_t* __restrict__ offs,
     const uint32_t* __restrict__ offs32, const GTile* __restrict__ gt) {
   __shared__ ScatterLds<LUT> L;
-  __shared__ alignas(16) uint16_t slut[LUT ? kLdsLutEntries : 8];
+  __shared__ alignas(16) uint16_t slut[kLutLdsEntries<LUT>];
   const int64_t t = xcd_remap(blockIdx.x, gridDim.x);
   const int ncols = desc->ncols;
   uint64_t v0[kScatterItems], v1[kScatterItems], v2[kScatterItems];
@@ -3302,15 +3319,18 @@ void launch_seg_map2(const int64_t* tbase, int64_t ntiles, int32_t* tile_seg,
 
 void launch_count(int key_size, const SortDesc* d, const SegPlan* plan,
                   const int32_t* tile_seg, int64_t ntiles, uint16_t* hist,
-                  unsigned long long* var_or, bool lut, hipStream_t st, const GTile* gt,
+                  unsigned long long* var_or, int lut, hipStream_t st, const GTile* gt,
                   const int32_t* torder) {
   const unsigned grid = (unsigned)((ntiles + kCountTiles - 1) / kCountTiles);
 #define CALL(KT, U, CZ)                                                                 \
-  if (lut)                                                                              \
-    count_kernel<KT, U, true, CZ><<<grid, kCountThreads, 0, st>>>(                       \
+  if (lut == 2)                                                                         \
+    count_kernel<KT, U, 2, CZ><<<grid, kCountThreads, 0, st>>>(                          \
+        d, plan, tile_seg, hist, var_or, gt, ntiles, torder);                           \
+  else if (lut)                                                                         \
+    count_kernel<KT, U, 1, CZ><<<grid, kCountThreads, 0, st>>>(                          \
         d, plan, tile_seg, hist, var_or, gt, ntiles, torder);                           \
   else                                                                                  \
-    count_kernel<KT, U, false, CZ><<<grid, kCountThreads, 0, st>>>(                      \
+    count_kernel<KT, U, 0, CZ><<<grid, kCountThreads, 0, st>>>(                          \
         d, plan, tile_seg, hist, var_or, gt, ntiles, torder)
   SRS_KEY_DISPATCH(key_size, CALL)
 #undef CALL
@@ -3342,23 +3362,26 @@ void launch_offsets(SegPlan* plan, int64_t nbig, const int32_t* group_seg, int64
 
 void launch_scatter(int key_size, const SortDesc* d, const SegPlan* plan,
                     const int32_t* tile_seg, const uint64_t* offs, const uint32_t* offs32,
-                    int64_t ntiles, bool lut, int ncols, hipStream_t st, const GTile* gt) {
+                    int64_t ntiles, int lut, int ncols, hipStream_t st, const GTile* gt) {
   const bool pre3 = ncols >= 3;
-#define CALL(KT, U, CZ)                                                                 \
-  if (lut && pre3)                                                                      \
-    scatter_kernel<KT, U, true, CZ, true><<<(unsigned)ntiles, kScatterThreads, 0, st>>>(  \
-        d, plan, tile_seg, offs, offs32, gt);                                               \
-  else if (lut)                                                                         \
-    scatter_kernel<KT, U, true, CZ, false><<<(unsigned)ntiles, kScatterThreads, 0, st>>>( \
-        d, plan, tile_seg, offs, offs32, gt);                                               \
-  else if (pre3)                                                                        \
-    scatter_kernel<KT, U, false, CZ, true><<<(unsigned)ntiles, kScatterThreads, 0, st>>>( \
-        d, plan, tile_seg, offs, offs32, gt);                                               \
+#define CALL_L(KT, U, CZ, LK)                                                           \
+  if (pre3)                                                                             \
+    scatter_kernel<KT, U, LK, CZ, true><<<(unsigned)ntiles, kScatterThreads, 0, st>>>(    \
+        d, plan, tile_seg, offs, offs32, gt);                                           \
   else                                                                                  \
-    scatter_kernel<KT, U, false, CZ, false><<<(unsigned)ntiles, kScatterThreads, 0, st>>>( \
+    scatter_kernel<KT, U, LK, CZ, false><<<(unsigned)ntiles, kScatterThreads, 0, st>>>(   \
         d, plan, tile_seg, offs, offs32, gt)
+#define CALL(KT, U, CZ)                                                                 \
+  if (lut == 2) {                                                                       \
+    CALL_L(KT, U, CZ, 2);                                                               \
+  } else if (lut) {                                                                     \
+    CALL_L(KT, U, CZ, 1);                                                               \
+  } else {                                                                              \
+    CALL_L(KT, U, CZ, 0);                                                               \
+  }
   SRS_KEY_DISPATCH(key_size, CALL)
 #undef CALL
+#undef CALL_L
 }
 
 void launch_stripe_tables(const uint32_t* prun, int64_t nstripes, int nb, uint32_t* ptile,
