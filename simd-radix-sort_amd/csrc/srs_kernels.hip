@@ -1335,7 +1335,7 @@ __global__ void stripe_gtile_kernel(const uint32_t* __restrict__ prun,
 template <int LUT>
 struct ScatterLds {
   uint64_t sval[kTile];
-  // digit of each staged slot (LUT passes recompute it instead: their 24 KB
+  // digit of each staged slot (big-table passes recompute it instead: their 24 KB
   // table must leave room for two workgroups per CU)
   uint16_t sdig[(LUT == 1 || !SRS_SCATTER_SDIG) ? 1 : kTile];
   alignas(8) uint16_t wc[kScatterThreads / 64][kMaxBins];  // zeroed as u64
@@ -1518,7 +1518,7 @@ __device__ __forceinline__ void scatter_process_tile(
       const uint32_t d = dg[k];
       pos[k] = L.bin_start[d] + L.wc[wave][d] + pos[k];
       L.sval[pos[k]] = v0[k];
-      if constexpr (!LUT && SRS_SCATTER_SDIG) L.sdig[pos[k]] = (uint16_t)d;
+      if constexpr (LUT != 1 && SRS_SCATTER_SDIG) L.sdig[pos[k]] = (uint16_t)d;
     }
   }
   lds_barrier();
