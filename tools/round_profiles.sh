@@ -8,7 +8,7 @@
 # usage: bash tools/round_profiles.sh <tag>
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 T=${1:-r03}
-bash tools/profile_round.sh $T --extra none || exit 1
+bash tools/profile_round.sh $T --extra none --cpu-sample 0 || exit 1
 bash tools/profile_round.sh ${T}c2 --config c2 --extra none --cpu-sample 0 || exit 1
 bash tools/profile_round.sh ${T}c3 --config c3 --extra none --cpu-sample 0 || exit 1
 echo "profiles done"
