@@ -308,6 +308,12 @@ int srs_debug_last_fallbacks(int64_t* counts);
  * Synchronizes the device. Tests use it to prove the direct kernel ran. */
 int srs_debug_last_local_counts(int64_t* counts);
 
+/* The same by LDS class: counts[0] / counts[1] = small (<= 4096 records) /
+ * large (<= 8192) segments of the local level, counts[2] / counts[3] = of
+ * those, the ones the direct kernel of the class handed to the fast kernel.
+ * Synchronizes the device. */
+int srs_debug_last_local_classes(int64_t* counts);
+
 /* Placement diagnostics. srs_debug_alloc allocates `bytes` of
  * device memory on the current device the way mode says (0 = hipMalloc,
  * 1 = physically contiguous, 2 = one hipMemCreate handle mapped at 1 GiB

@@ -61,6 +61,16 @@ bool direct_local_enabled() {
   return on;
 }
 
+// the large-class direct kernel (SRS_NO_DIRECT_LOCAL2=1: the fast kernel
+// takes the large class, for A/B runs)
+bool direct_local2_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("SRS_NO_DIRECT_LOCAL2");
+    return !(e && *e && *e != '0');
+  }();
+  return on;
+}
+
 // Fewest small-class segments for which the direct kernel runs. Below it the
 // fast kernel alone is cheaper: the direct kernel's hand-over list costs one
 // more launch (~5-9 us) per sort, and mid-size sorts of 8-byte keys keep more
@@ -420,7 +430,7 @@ struct Workspace {
   DevBuf tmp2;        // TMP2: AoS records as SoA slice columns (SortDesc::tmp2)
   DevBuf stage;       // device copy of host arrays (host-pointer API)
   DevBuf desc;        // SortDesc
-  DevBuf big[2], local, local2, copy, fallback, fallback2, redo;
+  DevBuf big[2], local, local2, copy, fallback, fallback2, redo, redo2;
   DevBuf plan, tcount, gcount, tbase, gbase, var, sbase;
   DevBuf tile_seg, group_seg, hist, offs, gsum, gofs, scan_tmp, totals, ctr;
   DevBuf shist, lut, lut_rbits;  // balanced first level (sampled histogram, digit table)
@@ -455,7 +465,7 @@ struct Workspace {
       (void)hipEventDestroy(idle);
     }
     DevBuf* bufs[] = {&tmp, &tmp2, &stage, &desc, &big[0], &big[1], &local, &local2, &fallback,
-                      &fallback2, &redo, &shist, &lut, &lut_rbits, &copy, &plan, &tcount,
+                      &fallback2, &redo, &redo2, &shist, &lut, &lut_rbits, &copy, &plan, &tcount,
                       &gcount, &tbase, &gbase, &var, &sbase, &tile_seg, &group_seg, &hist, &offs,
                       &gsum, &gofs, &scan_tmp, &totals, &ctr, &prun, &ptile, &btot, &bnt, &btile,
                       &nt_over, &gtile, &gorder};
@@ -796,13 +806,36 @@ void plan_table(const std::vector<uint32_t>& h, int64_t n, int key_bits, TablePl
   // table (up to 24 KB staged per tile, two dependent lookups).
   {
     const int kb = key_bits;
-    // bins worth less than one group share groups (consecutive, at most one
-    // share each): the tails of a float distribution would otherwise take a
-    // group per exponent
+    // A group's rbits bounds every key code the table sends it, so a group
+    // that takes a run of empty bins, or bins of different key density (two
+    // float exponents), gets a next digit that splits the keys it holds
+    // badly: C2's first group took the 128 empty bins below -1.0 (rbits 31)
+    // and left 1.95 M keys in one bucket, its shared tail group put one
+    // exponent's keys into a sixteenth of its buckets. When they fit, every
+    // non-empty bin gets groups of its own and every run of empty bins one
+    // group (which stays empty unless the sample missed keys). Otherwise bins
+    // worth less than one group share groups (consecutive, at most one share
+    // each) and empty bins join the group before them.
     std::vector<int> lg(512, -1);     // own groups 2^lg; -1: none
     std::vector<int> share(512, -1);  // >= 0: index of the shared group it joins
     int S = 0;
-    {
+    int nonempty = 0, empty_runs = 0;
+    for (int t = 0; t < 512; t++) {
+      nonempty += ct[t] != 0;
+      empty_runs += !ct[t] && (t == 0 || ct[t - 1]);
+    }
+    const bool own = nonempty + empty_runs <= 512;
+    if (own) {
+      S = empty_runs;
+      for (int t = 0; t < 512; t++) {
+        if (!ct[t]) continue;
+        const double x = 512.0 * (double)ct[t] / (double)total;
+        int l = 0;
+        while (l < 9 && (double)(2 << l) <= x * 1.4142) l++;  // (nearest power of two)
+        lg[t] = l;
+        S += 1 << l;
+      }
+    } else {
       double acc = 0;
       int nsh = 0;
       bool open = false;
@@ -863,7 +896,9 @@ void plan_table(const std::vector<uint32_t>& h, int64_t n, int key_bits, TablePl
       for (int t = 0; t < 512 && repr; t++) {
         if (lg[t] < 0) {
           int g;
-          if (share[t] >= 0 && share[t] != cur_share) {
+          if (own) {  // (an empty bin: its run's group)
+            g = (t == 0 || ct[t - 1]) ? run++ : run - 1;
+          } else if (share[t] >= 0 && share[t] != cur_share) {
             cur_share = share[t];
             g = run++;
           } else {
@@ -1183,11 +1218,24 @@ int run_level(Workspace* W, int ks, const SortDesc* d_desc, LevelState& S, int f
   S.n_local2 = (int64_t)W->h_ctr->n_local2;
   S.n_copy = (int64_t)W->h_ctr->n_copy;
   S.cur = nxt;
-  if (trace_levels())
+  if (trace_levels()) {
     fprintf(stderr, "[srs] level: %lld segs, %.0f keys, %lld tiles%s -> big %lld, local %lld, "
             "local2 %lld, copy %lld\n", (long long)nbig, level_elems, (long long)ntiles,
             lut ? " (lut)" : "", (long long)S.nbig, (long long)S.n_local,
             (long long)S.n_local2, (long long)S.n_copy);
+    if (S.nbig > 0) {  // the next level's segments: sizes and rbits
+      std::vector<Seg> b(S.nbig);
+      HIP_TRY(hipMemcpy(b.data(), W->big[nxt].p, S.nbig * sizeof(Seg), hipMemcpyDeviceToHost));
+      int64_t sum = 0, mx = 0, under16k = 0;
+      for (const Seg& s : b) {
+        sum += s.len;
+        mx = std::max<int64_t>(mx, s.len);
+        under16k += s.len <= 16384;
+      }
+      fprintf(stderr, "[srs]   big: %lld keys, max %lld, <= 16K keys: %lld segs; first rbits %d\n",
+              (long long)sum, (long long)mx, (long long)under16k, b[0].rbits);
+    }
+  }
   return SRS_OK;
 }
 
@@ -1644,19 +1692,29 @@ int run_sort(Workspace* W, const Request& R, hipStream_t st) {
     {
       TimedScope ts1("local_fast", 0, st);
       const bool rec16 = aos_cols && R.elem_size == 16;
-      if (n_local2 > 0)
-        launch_local(ksl, d_desc, (Seg*)W->local2.p, n_local2, 1, fb, nfb, st, rec16);
-      // the common shapes take the direct kernel at four workgroups per CU;
-      // what it hands over runs through the fast kernel:
-      // pm 0 a 4/8-byte key + one 8-byte payload (C1), 1 16-byte records of
-      // an 8-byte key as slices (C3), 2 a key + two 4-byte payloads (C2)
+      // the common shapes take the direct kernel at four workgroups per CU
+      // (two in the large class); what it hands over runs through the fast
+      // kernel: pm 0 a 4/8-byte key + one 8-byte payload (C1),
+      // 1 16-byte records of an 8-byte key as slices (C3), 2 a key + two
+      // 4-byte payloads (C2)
       int pm = -1;
       if (!R.aos && R.ncols == 2 && R.widths[1] == 8 && !d.tmp2) pm = 0;
       else if (rec16 && ks == 8) pm = 1;
       else if (d.pair && ks == 4) pm = 2;
       if (pm >= 0 && !direct_layout_ok(d, pm, ks)) pm = -1;  // (the kernel assumes it)
-      const bool direct = pm >= 0 && (ks == 4 || ks == 8) && !d.canon_zero &&
-                          direct_local_enabled() && n_local >= direct_min_segs();
+      const bool direct_any = pm >= 0 && (ks == 4 || ks == 8) && !d.canon_zero &&
+                              direct_local_enabled();
+      const bool direct = direct_any && n_local >= direct_min_segs();
+      const bool direct2 = direct_any && direct_local2_enabled() && n_local2 >= direct_min_segs();
+      if (n_local2 > 0 && direct2) {
+        SRS_TRY(ensure(W->redo2, n_local2 * sizeof(Seg)));
+        launch_local_direct(ks, pm, d_desc, (Seg*)W->local2.p, n_local2, (Seg*)W->redo2.p,
+                            &d_ctr->n_redo2, fb, nfb, st, true);
+        launch_local_list(ks, d_desc, (Seg*)W->redo2.p, &d_ctr->n_redo2,
+                          (int)std::min<int64_t>(n_local2, 1024), fb, nfb, st, true);
+      } else if (n_local2 > 0) {
+        launch_local(ksl, d_desc, (Seg*)W->local2.p, n_local2, 1, fb, nfb, st, rec16);
+      }
       if (n_local > 0 && direct) {
         SRS_TRY(ensure(W->redo, n_local * sizeof(Seg)));
         launch_local_direct(ks, pm, d_desc, (Seg*)W->local.p, n_local, (Seg*)W->redo.p,
@@ -1691,8 +1749,8 @@ int run_sort(Workspace* W, const Request& R, hipStream_t st) {
       fprintf(stderr, "[srs] local: %lld + %lld segs (%llu keys); stable fallback %llu + %llu, "
               "lsd fallback %llu\n", (long long)n_local, (long long)n_local2,
               c.local_elems, c.n_fallback1, c.n_fallback, c.n_fallback2);
-      fprintf(stderr, "[srs] local: %llu small-class segments handed from the direct kernel\n",
-              c.n_redo);
+      fprintf(stderr, "[srs] local: %llu + %llu small / large-class segments handed from the "
+              "direct kernel\n", c.n_redo, c.n_redo2);
     }
   }
   if (n_copy > 0) {
@@ -2653,7 +2711,24 @@ int srs_debug_last_local_counts(int64_t* counts) {
   ListCounters c;
   HIP_TRY(hipMemcpy(&c, W->ctr.p, sizeof c, hipMemcpyDeviceToHost));
   counts[0] = (int64_t)(c.n_local + c.n_local2);
-  counts[1] = (int64_t)c.n_redo;
+  counts[1] = (int64_t)(c.n_redo + c.n_redo2);
+  return SRS_OK;
+}
+
+int srs_debug_last_local_classes(int64_t* counts) {
+  if (!counts) return fail(SRS_ERR_INVALID_ARG, "counts is NULL");
+  Workspace* W = nullptr;
+  WsLock lk;
+  SRS_TRY(acquire_ws(&W, &lk));
+  counts[0] = counts[1] = counts[2] = counts[3] = 0;
+  if (W->last_small || !W->ctr.p) return SRS_OK;
+  HIP_TRY(hipDeviceSynchronize());
+  ListCounters c;
+  HIP_TRY(hipMemcpy(&c, W->ctr.p, sizeof c, hipMemcpyDeviceToHost));
+  counts[0] = (int64_t)c.n_local;
+  counts[1] = (int64_t)c.n_local2;
+  counts[2] = (int64_t)c.n_redo;
+  counts[3] = (int64_t)c.n_redo2;
   return SRS_OK;
 }
 

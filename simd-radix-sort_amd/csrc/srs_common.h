@@ -128,6 +128,7 @@ struct ListCounters {
   unsigned long long n_fallback1; // small-class segments handed to the stable kernel
   unsigned long long n_fallback2; // segments handed on to the LSD local kernel
   unsigned long long n_redo;      // small-class segments the direct kernel handed to the fast one
+  unsigned long long n_redo2;     // large-class segments the direct kernel handed to the fast one
 };
 
 // Tuning constants (see DESIGN.md §4 for how they were chosen).
@@ -210,6 +211,10 @@ constexpr int kLocalDirectItems = 4096 / kLocalDirectThreads;
 #define SRS_LOCAL_DIRECT_WGS_PER_CU 4
 #endif
 constexpr int kLocalDirectWavesPerEU = SRS_LOCAL_DIRECT_WGS_PER_CU * kLocalDirectThreads / 64 / 4;
+// and its large class (up to kLocalCap records): 2 workgroups of 512 x 16 per CU
+constexpr int kLocalDirectThreads2 = 512;
+constexpr int kLocalDirectItems2 = 8192 / kLocalDirectThreads2;
+constexpr int kLocalDirectWavesPerEU2 = 2 * kLocalDirectThreads2 / 64 / 4;
 // cache-policy bits of the scatter's / the direct local kernel's column
 // loads (buffer-load aux operand; 0 = default)
 #ifndef SRS_SCATTER_LOAD_AUX
@@ -263,7 +268,7 @@ __host__ __device__ inline int levels_for(int64_t len, int64_t target, int* need
 // small class's cost per key) instead of paying a count + scatter level and
 // its launches and host sync (C2's few oversized first-level groups: a
 // third and fourth level on ~1 % of the keys)
-constexpr int kLocalCapTarget = 7680;
+constexpr int kLocalCapTarget = 7808;
 
 __host__ __device__ inline int choose_bits(int64_t len, int rbits) {
   // bits needed to bring buckets under kLocalTarget, spread evenly over the

@@ -55,16 +55,17 @@ void launch_key_hist(int key_size, int64_t n, const void* keys, const SortDesc& 
 void launch_local(int key_size, const SortDesc* d, const Seg* segs, int64_t nsegs, int big_class,
                   Seg* fallback, unsigned long long* fallback_count, hipStream_t st,
                   bool rec16 = false);
-// the direct kernel (small class, no canon-zero, 4/8-byte keys; pm 0: one
-// 8-byte SoA payload, 1: 16-byte AoS records as slices, 2: desc->pair):
-// segments it does not take go to `redo`, large buckets to `fallback`;
-// launch_local_list then runs the fast kernel over `redo`
+// the direct kernel (no canon-zero, 4/8-byte keys; pm 0: one 8-byte SoA
+// payload, 1: 16-byte AoS records as slices, 2: desc->pair; big: the large
+// class, up to kLocalCap records): segments it does not take go to `redo`,
+// large buckets to `fallback`; launch_local_list then runs the fast kernel
+// of the same class over `redo`
 void launch_local_direct(int key_size, int pm, const SortDesc* d, const Seg* segs, int64_t nsegs,
                          Seg* redo, unsigned long long* redo_count, Seg* fallback,
-                         unsigned long long* fallback_count, hipStream_t st);
+                         unsigned long long* fallback_count, hipStream_t st, bool big = false);
 void launch_local_list(int key_size, const SortDesc* d, const Seg* segs,
                        const unsigned long long* nsegs, int grid, Seg* fallback,
-                       unsigned long long* fallback_count, hipStream_t st);
+                       unsigned long long* fallback_count, hipStream_t st, bool big = false);
 void launch_local_stable(int key_size, const SortDesc* d, const Seg* segs,
                          const unsigned long long* nsegs, int big_class, Seg* fallback,
                          unsigned long long* fallback_count, int grid, hipStream_t st);

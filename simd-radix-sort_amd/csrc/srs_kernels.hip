@@ -853,22 +853,27 @@ __device__ __forceinline__ void count_add(const SortDesc* __restrict__ desc,
     const bool ok0 = count_elem<KT>(T.vec, 0) < cnt;
     agg = __ballot(ok0 && d == d0) == __ballot(ok0);
   }
+  // No per-key branch or mask work: keys past the tile's end count into the
+  // spare bin kMaxBins (an earlier loop with `if (ok)` around each add cost
+  // C2's 4-byte count ~4x the VALU and ~8x the SALU instructions per key:
+  // 1.26 ms per launch against 0.74 for the same bytes in
+  // tools/probe/count_probe; SQ_INSTS_*, tools/prof_count.sh). `agg` is
+  // uniform, so its test per item is a scalar branch.
+  const bool full = cnt == kTile;
 #pragma unroll
   for (int k = 0; k < kCountItems; k++) {
-    const int e = count_elem<KT>(T.vec, k);
-    const bool ok = e < cnt;
+    const bool ok = full || count_elem<KT>(T.vec, k) < cnt;
     const U u = xf(raw[k]);
-    const uint32_t d = pass_digit<LUT>(u, P.shift, mask, lut);
-    if (ok) vor |= u ^ uref;
+    vor |= ok ? (U)(u ^ uref) : (U)0;
+    const uint32_t d = ok ? pass_digit<LUT>(u, P.shift, mask, lut) : (uint32_t)kMaxBins;
     if (agg) {
       const uint32_t d0 = __builtin_amdgcn_readfirstlane(d);
-      const uint64_t valid = __ballot(ok);
-      if (__ballot(ok && d == d0) == valid) {
-        if (valid && lane_id() == 0) atomicAdd(&h[d0], (uint32_t)__popcll(valid));
+      if (__ballot(d != d0) == 0) {  // (one digit, or none valid: d0 = kMaxBins)
+        if (lane_id() == 0) atomicAdd(&h[d0], (uint32_t)__popcll(__ballot(ok)));
         continue;
       }
     }
-    if (ok) atomicAdd(&h[d], 1u);
+    atomicAdd(&h[d], 1u);
   }
   if (vor) atomicOr(sor, (unsigned long long)vor);
 }
@@ -902,13 +907,19 @@ __device__ __forceinline__ void count_flush(const SegPlan* __restrict__ plan, co
 }
 
 template <typename KT, typename U, int LUT, bool CZ>
-__global__ __launch_bounds__(kCountThreads) void count_kernel(
+#ifndef SRS_COUNT_WPE
+#define SRS_COUNT_LB __launch_bounds__(kCountThreads)
+#else  // (tuning: force the count's waves per SIMD)
+#define SRS_COUNT_LB __launch_bounds__(kCountThreads, SRS_COUNT_WPE)
+#endif
+__global__ SRS_COUNT_LB void count_kernel(
     const SortDesc* __restrict__ desc, const SegPlan* __restrict__ plan,
     const int32_t* __restrict__ tile_seg, uint16_t* __restrict__ hist,
     unsigned long long* __restrict__ var_or, const GTile* __restrict__ gt, int64_t ntiles,
     const int32_t* __restrict__ torder) {
   constexpr int NH = kCountTiles > 1 ? 2 : 1;  // (one row when nothing is prefetched:
-  __shared__ uint32_t h[NH][kMaxBins];          //  the LUT pass keeps 6 workgroups per CU)
+  __shared__ uint32_t h[NH][kMaxBins + 16];     //  the LUT pass keeps 6 workgroups per CU;
+                                                //  bin kMaxBins: keys past the tile's end)
   __shared__ unsigned long long sh_or[NH];
   int64_t t0 = xcd_remap(blockIdx.x, gridDim.x) * kCountTiles;
   // gathered level: tiles in stripe order (each stripe's pieces lie back to
@@ -919,7 +930,7 @@ __global__ __launch_bounds__(kCountThreads) void count_kernel(
   U ua, ub;
   CountTile A = count_load<KT, U>(desc, plan, tile_seg, gt, t0, ntiles, ra, ua);
   const DigitLut lut = stage_lut<LUT, kCountThreads>(desc, slut);
-  for (uint32_t i = threadIdx.x; i < NH * kMaxBins; i += kCountThreads) (&h[0][0])[i] = 0;
+  for (uint32_t i = threadIdx.x; i < NH * (kMaxBins + 16); i += kCountThreads) (&h[0][0])[i] = 0;
   if (threadIdx.x < NH) sh_or[threadIdx.x] = 0;
   lds_barrier();
 #pragma unroll
@@ -2331,8 +2342,8 @@ __global__ __launch_bounds__(NT, WPE) void local_direct_kernel(
     unsigned long long* redo_count, Seg* __restrict__ fallback,
     unsigned long long* fallback_count, int xcd) {
   constexpr int CAP = NT * IT;
-  constexpr int IDXB = 12;
-  static_assert(CAP <= (1 << IDXB), "index bits");
+  constexpr int IDXB = CAP <= 4096 ? 12 : 13;  // bits of an index inside the segment
+  static_assert(CAP <= (1 << IDXB) && CAP <= 65536, "index bits, u16 cursors");
   constexpr int NB = 1 << kLocalTopBits;
   constexpr int NW = NT / 64;
   constexpr int BPT = NB / NT;  // bins per thread (an even count: packed pairs)
@@ -3423,28 +3434,46 @@ void launch_local(int key_size, const SortDesc* d, const Seg* segs, int64_t nseg
 
 void launch_local_direct(int key_size, int pm, const SortDesc* d, const Seg* segs,
                          int64_t nsegs, Seg* redo, unsigned long long* redo_count, Seg* fallback,
-                         unsigned long long* fallback_count, hipStream_t st) {
+                         unsigned long long* fallback_count, hipStream_t st, bool big) {
 #define CALL(KT, PM)                                                                          \
-  local_direct_kernel<KT, KT, kLocalDirectThreads, kLocalDirectItems, kLocalDirectWavesPerEU, \
-                      PM><<<(unsigned)nsegs, kLocalDirectThreads, 0, st>>>(                   \
-      d, segs, redo, redo_count, fallback, fallback_count, xcd)
+  if (big)                                                                                    \
+    local_direct_kernel<KT, KT, kLocalDirectThreads2, kLocalDirectItems2,                     \
+                        kLocalDirectWavesPerEU2, PM>                                          \
+        <<<(unsigned)nsegs, kLocalDirectThreads2, 0, st>>>(d, segs, redo, redo_count,         \
+                                                           fallback, fallback_count, xcd);    \
+  else                                                                                        \
+    local_direct_kernel<KT, KT, kLocalDirectThreads, kLocalDirectItems,                       \
+                        kLocalDirectWavesPerEU, PM>                                           \
+        <<<(unsigned)nsegs, kLocalDirectThreads, 0, st>>>(d, segs, redo, redo_count,          \
+                                                          fallback, fallback_count, xcd)
   // consecutive list entries on one XCD (SRS_LOCAL_XCD=0: plain order, for
   // A/B runs): C1 local 6.19-6.24 ms vs 5.95-6.56 in list order, same box
   static const int xcd = [] {
     const char* e = getenv("SRS_LOCAL_XCD");
     return (e && *e == '0') ? 0 : 1;
   }();
-  if (pm == 1) CALL(uint64_t, 1);
-  else if (pm == 2) CALL(uint32_t, 2);
-  else if (key_size == 4) CALL(uint32_t, 0);
-  else CALL(uint64_t, 0);
+  if (pm == 1) {
+    CALL(uint64_t, 1);
+  } else if (pm == 2) {
+    CALL(uint32_t, 2);
+  } else if (key_size == 4) {
+    CALL(uint32_t, 0);
+  } else {
+    CALL(uint64_t, 0);
+  }
 #undef CALL
 }
 
 void launch_local_list(int key_size, const SortDesc* d, const Seg* segs,
                        const unsigned long long* nsegs, int grid, Seg* fallback,
-                       unsigned long long* fallback_count, hipStream_t st) {
-  if (key_size == 4)
+                       unsigned long long* fallback_count, hipStream_t st, bool big) {
+  if (big && key_size == 4)
+    local_list_kernel<uint32_t, uint32_t, kLocalThreads, kLocalItems, kLocalWavesPerEU>
+        <<<(unsigned)grid, kLocalThreads, 0, st>>>(d, segs, nsegs, fallback, fallback_count);
+  else if (big)
+    local_list_kernel<uint64_t, uint64_t, kLocalThreads, kLocalItems, kLocalWavesPerEU>
+        <<<(unsigned)grid, kLocalThreads, 0, st>>>(d, segs, nsegs, fallback, fallback_count);
+  else if (key_size == 4)
     local_list_kernel<uint32_t, uint32_t, kLocalThreadsSmall, kLocalItemsSmall,
                       kLocalWavesPerEUSmall>
         <<<(unsigned)grid, kLocalThreadsSmall, 0, st>>>(d, segs, nsegs, fallback, fallback_count);
@@ -3595,6 +3624,7 @@ __device__ __forceinline__ void init_lists_body(Seg seg0, int to_local, Seg* big
     ctr->n_fallback1 = 0;
     ctr->n_fallback2 = 0;
     ctr->n_redo = 0;
+    ctr->n_redo2 = 0;
     ctr->local_elems = to_local ? (unsigned long long)seg0.len : 0;
     if (to_local) (small ? local : local2)[0] = seg0; else big[0] = seg0;
   }

@@ -81,6 +81,7 @@ def lib() -> ctypes.CDLL:
                                        ctypes.c_int, vp, i32, vp, vp, vp, vp]
     L.srs_debug_last_fallbacks.argtypes = [ctypes.POINTER(i64)]
     L.srs_debug_last_local_counts.argtypes = [ctypes.POINTER(i64)]
+    L.srs_debug_last_local_classes.argtypes = [ctypes.POINTER(i64)]
     L.srs_set_host_devices.argtypes = [i32, vp]
     L.srs_last_error.restype = ctypes.c_char_p
     L.srs_version.restype = ctypes.c_char_p
@@ -387,6 +388,15 @@ def last_local_counts():
     c = (ctypes.c_int64 * 2)()
     _check(lib().srs_debug_last_local_counts(c))
     return int(c[0]), int(c[1])
+
+
+def last_local_classes():
+    """(small-class segments, large-class segments, of each the ones the
+    direct kernel handed to the fast kernel) of the last sort on the current
+    device (synchronizes the device)."""
+    c = (ctypes.c_int64 * 4)()
+    _check(lib().srs_debug_last_local_classes(c))
+    return tuple(int(x) for x in c)
 
 
 class _DeviceBlock:

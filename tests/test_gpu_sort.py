@@ -244,7 +244,10 @@ def test_local_fallback_paths(case, n):
 @pytest.mark.parametrize("shape", ["u64+u64", "u32+u64", "i64+u64-down",
                                    "f32+2xu32", "f32+2xu32-dups", "i32+2xu32-down",
                                    "rec16-u64", "rec16-f64-down", "u64+u64-exact",
-                                   "u64+u64-equal", "u64+u64-wide", "u64+u64-nosort"])
+                                   "u64+u64-equal", "u64+u64-wide", "u64+u64-nosort",
+                                   "u64+u64-large", "u32+u64-large", "i32+2xu32-large",
+                                   "i32+2xu32-dups-large", "rec16-u64-large",
+                                   "u64+u64-down-large"])
 def test_direct_local_kernel(shape):
     """The direct local kernel (4 workgroups of 256 x 16 per CU)
     takes every local segment of the common shapes -- a 4/8-byte key with one
@@ -258,7 +261,11 @@ def test_direct_local_kernel(shape):
     to 55 varying bits of full-range keys, and (key bits, index) words of
     more than 52 key bits go to the fast kernel's wide mode ('-wide').
     Segments of few varying bits ('-exact', '-equal': 3000 copies of each
-    value) go to the fast kernel's exact pass, except in the pair mode."""
+    value) go to the fast kernel's exact pass, except in the pair mode.
+    '-large': ~5.9K records per local segment (uniform integer keys: float
+    keys spread unevenly over the first level's buckets), the large LDS class
+    (512 x 16 per workgroup, two per CU); srs_debug_last_local_classes proves
+    that class took them."""
     import os
     os.environ["SRS_DIRECT_MIN_SEGS"] = "1"  # (by default only sorts of >= 8192 local segments)
     try:
@@ -267,9 +274,21 @@ def test_direct_local_kernel(shape):
         del os.environ["SRS_DIRECT_MIN_SEGS"]
 
 
+def _check_local_class(large):
+    """-large: the large class took most segments, and its direct kernel
+    handed (almost) none of them to the fast kernel."""
+    if not large:
+        return
+    small, big, redo_small, redo_big = srs_amd.last_local_classes()
+    assert big > small and redo_big * 100 <= big, (small, big, redo_small, redo_big)
+
+
 def _direct_local_case(shape):
-    n = (1 << 21) + 77
     rng = np.random.default_rng(sum(map(ord, shape)))
+    large = shape.endswith("-large")
+    shape = shape[:-len("-large")] if large else shape
+    # (-large: one global level of 512 buckets leaves ~5.9K keys per bucket)
+    n = 3_000_077 if large else (1 << 21) + 77
     up = not shape.endswith("-down")
     idx = np.arange(n, dtype=np.uint64)
     if shape.startswith("rec16"):
@@ -284,12 +303,15 @@ def _direct_local_case(shape):
         e = elems.copy()
         srs_amd.sort_combined(e, kind, up=up)
         nloc, redo = srs_amd.last_local_counts()
+        _check_local_class(large)
         assert bytes_equal(e, stable_aos(kind, up, elems))
         assert nloc > 0 and redo * 100 <= nloc, (nloc, redo)
         return
     if "2xu32" in shape:
         kind = 5 if shape.startswith("i32") else 8
-        if shape.endswith("-dups"):
+        if shape.endswith("-dups") and kind == 5:  # 2^16 values, ~46 copies each (-large)
+            keys = (rng.integers(-(1 << 15), 1 << 15, n) << 16).astype(np.int32)
+        elif shape.endswith("-dups"):
             keys = (rng.integers(-(1 << 15), 1 << 15, n) / 32768.0).astype(np.float32)
         else:
             keys = make_keys(kind, "uniform", n, 9)
@@ -298,6 +320,7 @@ def _direct_local_case(shape):
         k, a, b = keys.copy(), p0.copy(), p1.copy()
         srs_amd.sort(k, a, b, up=up)
         nloc, redo = srs_amd.last_local_counts()
+        _check_local_class(large)
         st = stable_reference(kind, up, [keys, p0, p1])
         assert bytes_equal(k, st[0]) and bytes_equal(a, st[1]) and bytes_equal(b, st[2])
         # (a few segments may never have left the input arrays, where the
@@ -321,6 +344,7 @@ def _direct_local_case(shape):
     else:
         srs_amd.sort(k, p, up=up)
     nloc, redo = srs_amd.last_local_counts()
+    _check_local_class(large)
     assert nloc > 0
     if shape.endswith("-equal") or shape.endswith("-exact"):
         pass  # (few values per segment, or one: either kernel may take them)

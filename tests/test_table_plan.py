@@ -117,3 +117,18 @@ def test_spread_keys_need_no_table():
     mode, groups, over, other, table, rbits = _plan(hist, 10 ** 9, 64)
     if mode:
         _check_groups(mode, table, rbits, u, 64)
+
+
+def test_c2_sorts_in_two_global_levels():
+    """C2 (BASELINE configs[2]) takes two global levels: replaying the levels
+    on the exact per-value key counts (tools/c2_levels.py: the planner's table,
+    then the kernels' digit choice per segment) leaves no segment above the
+    LDS capacity after level 2. Round 3's table left 2,101 such buckets
+    (third and fourth levels): a group that took the empty bins below -1.0
+    got rbits 31, so its next digit split nothing."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "tools"))
+    from c2_levels import simulate
+    levels = simulate(10 ** 9, verbose=False)
+    assert len(levels) >= 2 and levels[1] == (0, 0), levels
