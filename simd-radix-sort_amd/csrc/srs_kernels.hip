@@ -858,22 +858,33 @@ __device__ __forceinline__ void count_add(const SortDesc* __restrict__ desc,
   // C2's 4-byte count ~4x the VALU and ~8x the SALU instructions per key:
   // 1.26 ms per launch against 0.74 for the same bytes in
   // tools/probe/count_probe; SQ_INSTS_*, tools/prof_count.sh). `agg` is
-  // uniform, so its test per item is a scalar branch.
+  // uniform: the two loops are separate code (a per-item test of it left
+  // ~20 scalar instructions per item in the mixed-digit loop).
   const bool full = cnt == kTile;
-#pragma unroll
-  for (int k = 0; k < kCountItems; k++) {
-    const bool ok = full || count_elem<KT>(T.vec, k) < cnt;
+  auto digit_of = [&](int k, bool& ok) -> uint32_t {
+    ok = full || count_elem<KT>(T.vec, k) < cnt;
     const U u = xf(raw[k]);
     vor |= ok ? (U)(u ^ uref) : (U)0;
-    const uint32_t d = ok ? pass_digit<LUT>(u, P.shift, mask, lut) : (uint32_t)kMaxBins;
-    if (agg) {
+    return ok ? pass_digit<LUT>(u, P.shift, mask, lut) : (uint32_t)kMaxBins;
+  };
+  if (!agg) {
+#pragma unroll
+    for (int k = 0; k < kCountItems; k++) {
+      bool ok;
+      atomicAdd(&h[digit_of(k, ok)], 1u);
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < kCountItems; k++) {
+      bool ok;
+      const uint32_t d = digit_of(k, ok);
       const uint32_t d0 = __builtin_amdgcn_readfirstlane(d);
       if (__ballot(d != d0) == 0) {  // (one digit, or none valid: d0 = kMaxBins)
         if (lane_id() == 0) atomicAdd(&h[d0], (uint32_t)__popcll(__ballot(ok)));
-        continue;
+      } else {
+        atomicAdd(&h[d], 1u);
       }
     }
-    atomicAdd(&h[d], 1u);
   }
   if (vor) atomicOr(sor, (unsigned long long)vor);
 }
@@ -906,13 +917,14 @@ __device__ __forceinline__ void count_flush(const SegPlan* __restrict__ plan, co
   }
 }
 
+// waves per SIMD the compiler must keep: 8 for the small-table passes (the
+// 8-byte range level otherwise lands at 105 SGPRs, 7 waves; the cost is 26
+// SGPRs spilled to VGPR lanes), no constraint elsewhere (forcing 8 on C1's
+// plain pass spills 24 SGPRs it does not need to)
+template <int LUT>
+constexpr int kCountMinWaves = LUT == 2 ? 8 : 1;
 template <typename KT, typename U, int LUT, bool CZ>
-#ifndef SRS_COUNT_WPE
-#define SRS_COUNT_LB __launch_bounds__(kCountThreads)
-#else  // (tuning: force the count's waves per SIMD)
-#define SRS_COUNT_LB __launch_bounds__(kCountThreads, SRS_COUNT_WPE)
-#endif
-__global__ SRS_COUNT_LB void count_kernel(
+__global__ __launch_bounds__(kCountThreads, kCountMinWaves<LUT>) void count_kernel(
     const SortDesc* __restrict__ desc, const SegPlan* __restrict__ plan,
     const int32_t* __restrict__ tile_seg, uint16_t* __restrict__ hist,
     unsigned long long* __restrict__ var_or, const GTile* __restrict__ gt, int64_t ntiles,
