@@ -1109,7 +1109,7 @@ int run_level(Workspace* W, int ks, const SortDesc* d_desc, LevelState& S, int f
   SRS_TRY(ensure(W->gcount, nbig * 8));
   SRS_TRY(ensure(W->tbase, nbig * 8));
   SRS_TRY(ensure(W->gbase, nbig * 8));
-  SRS_TRY(ensure(W->var, nbig * 8));
+  SRS_TRY(ensure(W->var, nbig * 16));  // the segments' key OR, then their key AND
   SRS_TRY(ensure(W->sbase, (size_t)nbig * kMaxBins * 8));
   SRS_TRY(ensure(W->scan_tmp, scan_temp_elems(nbig) * 8));
   SegPlan* plan = (SegPlan*)W->plan.p;
@@ -1169,8 +1169,8 @@ int run_level(Workspace* W, int ks, const SortDesc* d_desc, LevelState& S, int f
                   group_seg, nbig, st);
   {
     TimedScope ts("count", (double)0, st, lv);
-    launch_count(ks, d_desc, plan, tile_seg, ntiles, (uint16_t*)W->hist.p, var, lut, st, M.gt,
-                 M.torder);
+    launch_count(ks, d_desc, plan, tile_seg, ntiles, (uint16_t*)W->hist.p, var, var + nbig, lut, st,
+                 M.gt, M.torder);
   }
   // ---- offsets + children (list capacity for the worst case: every bin non-empty)
   const size_t worst = (size_t)nbig * kMaxBins;

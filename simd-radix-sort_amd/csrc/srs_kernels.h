@@ -25,8 +25,8 @@ void launch_plan_bases(SegPlan* plan, int64_t nbig, const int64_t* tbase,
                        const int64_t* gbase, hipStream_t st);
 void launch_count(int key_size, const SortDesc* d, const SegPlan* plan,
                   const int32_t* tile_seg, int64_t ntiles, uint16_t* hist,
-                  unsigned long long* var_or, int lut, hipStream_t st,
-                  const GTile* gt = nullptr, const int32_t* torder = nullptr);
+                  unsigned long long* var_or, unsigned long long* var_and, int lut,
+                  hipStream_t st, const GTile* gt = nullptr, const int32_t* torder = nullptr);
 int64_t scan_temp_elems(int64_t n);
 void launch_excl_scan(const uint64_t* x, uint64_t* y, int64_t n, uint64_t* temp,
                       uint64_t* total, hipStream_t st);

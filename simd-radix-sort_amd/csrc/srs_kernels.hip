@@ -525,7 +525,8 @@ __global__ void plan_kernel(const Seg* __restrict__ big, int64_t nbig,
   plan[s] = p;
   tcount[s] = p.ntiles;
   gcount[s] = p.ngroups;
-  var_or[s] = 0;
+  var_or[s] = 0;            // OR of the segment's (transformed) keys
+  var_or[nbig + s] = ~0ull;  // and their AND (count_flush)
 }
 
 // Few segments (nbig <= kPlanSmallMax): the whole plan step in one
@@ -565,6 +566,7 @@ __global__ __launch_bounds__(kPlanSmallThreads) void plan_small_kernel(
       tbase[s] = p.tile_base;
       gbase[s] = p.group_base;
       var_or[s] = 0;
+      var_or[nbig + s] = ~0ull;
     }
     tc += tt;
     gc += gt;
@@ -758,14 +760,13 @@ __device__ __forceinline__ int count_elem(bool vec, int k) {
              : k * kCountThreads + (int)threadIdx.x;
 }
 
-// Issues tile t's key loads (raw) and its segment's reference key (uref_raw).
+// Issues tile t's key loads (raw).
 template <typename KT, typename U>
 __device__ __forceinline__ CountTile count_load(const SortDesc* __restrict__ desc,
                                                 const SegPlan* __restrict__ plan,
                                                 const int32_t* __restrict__ tile_seg,
                                                 const GTile* __restrict__ gt, int64_t t,
-                                                int64_t ntiles, U (&raw)[kCountItems],
-                                                U& uref_raw) {
+                                                int64_t ntiles, U (&raw)[kCountItems]) {
   CountTile T;
   T.t = t;
   T.cnt = 0;
@@ -774,26 +775,22 @@ __device__ __forceinline__ CountTile count_load(const SortDesc* __restrict__ des
   if (t >= ntiles) {
 #pragma unroll
     for (int k = 0; k < kCountItems; k++) raw[k] = 0;
-    uref_raw = 0;
     return T;
   }
   T.s = tile_seg[t];
   const SegPlan P = plan[T.s];
   const char* kp = desc->key.base[P.buf];
   const uint32_t ks = desc->key.stride[P.buf];
-  int64_t base, first;
+  int64_t base;
   if (gt) {  // gathered level: the tile table says where the records are
     base = gt[t].src;
     T.cnt = gt[t].cnt;
-    first = gt[P.tile_base].src;  // one reference key per segment
   } else {
     const int64_t tl = t - P.tile_base;
     base = P.start + tl * kTile;
     const int64_t rem = P.len - tl * kTile;
     T.cnt = rem < kTile ? (int)rem : kTile;
-    first = P.start;
   }
-  uref_raw = (U)gld<KT>(kp + first * (int64_t)ks);
   constexpr int KB = (int)sizeof(KT);
   constexpr int PER = KB >= 4 ? 16 / KB : 1;
   static_assert(kCountItems % PER == 0, "whole 16-byte pieces per thread");
@@ -830,7 +827,7 @@ __device__ __forceinline__ CountTile count_load(const SortDesc* __restrict__ des
 template <typename KT, typename U, int LUT, bool CZ>
 __device__ __forceinline__ void count_add(const SortDesc* __restrict__ desc,
                                           const SegPlan* __restrict__ plan, const CountTile& T,
-                                          const U (&raw)[kCountItems], U uref_raw,
+                                          const U (&raw)[kCountItems],
                                           uint32_t* h, unsigned long long* sor,
                                           const DigitLut& lut) {
   if (T.cnt == 0) return;
@@ -838,9 +835,11 @@ __device__ __forceinline__ void count_add(const SortDesc* __restrict__ desc,
   const uint32_t mask = (1u << P.bits) - 1;
   Xform<U, CZ> xf;
   xf.init(*desc);
-  const U uref = xf(uref_raw);
   const int cnt = T.cnt;
-  U vor = 0;
+  // the segment's varying bits are OR(keys) ^ AND(keys): no reference key
+  // (loading the segment's first key put a dependent load in front of every
+  // tile: C2's 4-byte counts 1.25 / 1.10 -> 0.85 ms without it)
+  U vor = 0, vand = ~(U)0;
   // A wave holds 64 consecutive keys. Sorted or constant inputs give it one
   // digit, and 64 lanes adding into one LDS counter serialise (sorted C1
   // input: 3.6 ms per count launch against 1.45 uniform). A wave whose valid
@@ -864,7 +863,8 @@ __device__ __forceinline__ void count_add(const SortDesc* __restrict__ desc,
   auto digit_of = [&](int k, bool& ok) -> uint32_t {
     ok = full || count_elem<KT>(T.vec, k) < cnt;
     const U u = xf(raw[k]);
-    vor |= ok ? (U)(u ^ uref) : (U)0;
+    vor |= ok ? u : (U)0;
+    vand &= ok ? u : ~(U)0;
     return ok ? pass_digit<LUT>(u, P.shift, mask, lut) : (uint32_t)kMaxBins;
   };
   if (!agg) {
@@ -879,14 +879,25 @@ __device__ __forceinline__ void count_add(const SortDesc* __restrict__ desc,
       bool ok;
       const uint32_t d = digit_of(k, ok);
       const uint32_t d0 = __builtin_amdgcn_readfirstlane(d);
-      if (__ballot(d != d0) == 0) {  // (one digit, or none valid: d0 = kMaxBins)
-        if (lane_id() == 0) atomicAdd(&h[d0], (uint32_t)__popcll(__ballot(ok)));
+      const uint64_t vm = __ballot(ok);  // (all lanes: a ballot inside `lane 0` sees one)
+      if (__ballot(d != d0) == 0) {      // (one digit, or none valid: d0 = kMaxBins)
+        if (lane_id() == 0) atomicAdd(&h[d0], (uint32_t)__popcll(vm));
       } else {
         atomicAdd(&h[d], 1u);
       }
     }
   }
-  if (vor) atomicOr(sor, (unsigned long long)vor);
+  // one LDS atomic pair per wave (sor[0]: OR, sor[1]: AND; U's upper bits
+  // are 0 in both, i.e. not varying)
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    vor |= __shfl_xor(vor, o, 64);
+    vand &= __shfl_xor(vand, o, 64);
+  }
+  if (lane_id() == 0) {
+    atomicOr(&sor[0], (unsigned long long)vor);
+    atomicAnd(&sor[1], (unsigned long long)vand);
+  }
 }
 
 // After a barrier: the tile's row of u16 counts (a tile holds <= kTile = 4096
@@ -895,7 +906,8 @@ __device__ __forceinline__ void count_add(const SortDesc* __restrict__ desc,
 __device__ __forceinline__ void count_flush(const SegPlan* __restrict__ plan, const CountTile& T,
                                             uint32_t* h, unsigned long long* sor,
                                             uint16_t* __restrict__ hist,
-                                            unsigned long long* __restrict__ var_or) {
+                                            unsigned long long* __restrict__ var_or,
+                                            unsigned long long* __restrict__ var_and) {
   static_assert(kTile < 65536, "u16 tile counts");
   if (T.cnt == 0) return;
   const uint32_t nb = 1u << plan[T.s].bits;
@@ -906,57 +918,64 @@ __device__ __forceinline__ void count_flush(const SegPlan* __restrict__ plan, co
     h[2 * i + 1] = 0;
   }
   if (threadIdx.x == 0) {
-    const unsigned long long o = *sor;
-    *sor = 0;
-    if (o) {
-      // most tiles add no new bits: skip the (contended) atomic then
-      const unsigned long long known =
-          __hip_atomic_load(&var_or[T.s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (o & ~known) atomicOr(&var_or[T.s], o);
-    }
+    const unsigned long long o = sor[0], a = sor[1];
+    sor[0] = 0;
+    sor[1] = ~0ull;
+    // most tiles add nothing new: skip the (contended) atomics then
+    const unsigned long long ko =
+        __hip_atomic_load(&var_or[T.s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (o & ~ko) atomicOr(&var_or[T.s], o);
+    const unsigned long long ka =
+        __hip_atomic_load(&var_and[T.s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (ka & ~a) atomicAnd(&var_and[T.s], a);
   }
 }
 
-// waves per SIMD the compiler must keep: 8 for the small-table passes (the
-// 8-byte range level otherwise lands at 105 SGPRs, 7 waves; the cost is 26
-// SGPRs spilled to VGPR lanes), no constraint elsewhere (forcing 8 on C1's
-// plain pass spills 24 SGPRs it does not need to)
-template <int LUT>
-constexpr int kCountMinWaves = LUT == 2 ? 8 : 1;
+// waves per SIMD the compiler must keep: 8 for the small-table passes of
+// keys up to 4 bytes (C2's first level lands at 7 otherwise), no constraint
+// elsewhere (forcing 8 on C1's plain pass spills 24 SGPRs it does not need
+// to; on the 8-byte range level it spills 30-54 VGPRs to scratch: that one
+// runs at 7 waves)
+template <int LUT, int KB>
+constexpr int kCountMinWaves = LUT == 2 && KB <= 4 ? 8 : 1;
 template <typename KT, typename U, int LUT, bool CZ>
-__global__ __launch_bounds__(kCountThreads, kCountMinWaves<LUT>) void count_kernel(
+__global__ __launch_bounds__(kCountThreads, (kCountMinWaves<LUT, (int)sizeof(KT)>)) void count_kernel(
     const SortDesc* __restrict__ desc, const SegPlan* __restrict__ plan,
     const int32_t* __restrict__ tile_seg, uint16_t* __restrict__ hist,
-    unsigned long long* __restrict__ var_or, const GTile* __restrict__ gt, int64_t ntiles,
-    const int32_t* __restrict__ torder) {
+    unsigned long long* __restrict__ var_or, unsigned long long* __restrict__ var_and,
+    const GTile* __restrict__ gt, int64_t ntiles, const int32_t* __restrict__ torder) {
   constexpr int NH = kCountTiles > 1 ? 2 : 1;  // (one row when nothing is prefetched:
   __shared__ uint32_t h[NH][kMaxBins + 16];     //  the LUT pass keeps 6 workgroups per CU;
                                                 //  bin kMaxBins: keys past the tile's end)
-  __shared__ unsigned long long sh_or[NH];
+  __shared__ unsigned long long sh_or[NH][2];  // the tile's key OR and AND
   int64_t t0 = xcd_remap(blockIdx.x, gridDim.x) * kCountTiles;
   // gathered level: tiles in stripe order (each stripe's pieces lie back to
   // back, so the reads sweep memory); the rows do not depend on the order
+#ifndef SRS_DIAG_COUNT_NOTORDER
   if (torder && kCountTiles == 1) t0 = torder[t0];
+#endif
   __shared__ alignas(16) uint16_t slut[kLutLdsEntries<LUT>];
   U ra[kCountItems], rb[kCountItems];
-  U ua, ub;
-  CountTile A = count_load<KT, U>(desc, plan, tile_seg, gt, t0, ntiles, ra, ua);
+  CountTile A = count_load<KT, U>(desc, plan, tile_seg, gt, t0, ntiles, ra);
   const DigitLut lut = stage_lut<LUT, kCountThreads>(desc, slut);
   for (uint32_t i = threadIdx.x; i < NH * (kMaxBins + 16); i += kCountThreads) (&h[0][0])[i] = 0;
-  if (threadIdx.x < NH) sh_or[threadIdx.x] = 0;
+  if (threadIdx.x < NH) {
+    sh_or[threadIdx.x][0] = 0;
+    sh_or[threadIdx.x][1] = ~0ull;
+  }
   lds_barrier();
 #pragma unroll
   for (int i = 0; i < kCountTiles; i += 2) {
     CountTile B;
-    if (i + 1 < kCountTiles) B = count_load<KT, U>(desc, plan, tile_seg, gt, t0 + i + 1, ntiles, rb, ub);
-    count_add<KT, U, LUT, CZ>(desc, plan, A, ra, ua, h[0], &sh_or[0], lut);
+    if (i + 1 < kCountTiles) B = count_load<KT, U>(desc, plan, tile_seg, gt, t0 + i + 1, ntiles, rb);
+    count_add<KT, U, LUT, CZ>(desc, plan, A, ra, h[0], &sh_or[0][0], lut);
     lds_barrier();
-    count_flush(plan, A, h[0], &sh_or[0], hist, var_or);
+    count_flush(plan, A, h[0], &sh_or[0][0], hist, var_or, var_and);
     if (i + 1 < kCountTiles) {
-      if (i + 2 < kCountTiles) A = count_load<KT, U>(desc, plan, tile_seg, gt, t0 + i + 2, ntiles, ra, ua);
-      count_add<KT, U, LUT, CZ>(desc, plan, B, rb, ub, h[NH - 1], &sh_or[NH - 1], lut);
+      if (i + 2 < kCountTiles) A = count_load<KT, U>(desc, plan, tile_seg, gt, t0 + i + 2, ntiles, ra);
+      count_add<KT, U, LUT, CZ>(desc, plan, B, rb, h[NH - 1], &sh_or[NH - 1][0], lut);
       lds_barrier();
-      count_flush(plan, B, h[NH - 1], &sh_or[NH - 1], hist, var_or);
+      count_flush(plan, B, h[NH - 1], &sh_or[NH - 1][0], hist, var_or, var_and);
     }
   }
 }
@@ -1170,7 +1189,7 @@ __global__ __launch_bounds__(kMaxBins) void seg_scan_kernel(
   if (single) {
     if (b == 0) {
       plan[s].skip = 1;
-      const unsigned long long v = var_or[s];
+      const unsigned long long v = var_or[s] ^ var_or[gridDim.x + s];  // OR ^ AND of the keys
       c.start = P.start;
       c.len = P.len;
       c.rbits = v ? 64 - __clzll((long long)v) : 0;
@@ -3342,19 +3361,19 @@ void launch_seg_map2(const int64_t* tbase, int64_t ntiles, int32_t* tile_seg,
 
 void launch_count(int key_size, const SortDesc* d, const SegPlan* plan,
                   const int32_t* tile_seg, int64_t ntiles, uint16_t* hist,
-                  unsigned long long* var_or, int lut, hipStream_t st, const GTile* gt,
-                  const int32_t* torder) {
+                  unsigned long long* var_or, unsigned long long* var_and, int lut,
+                  hipStream_t st, const GTile* gt, const int32_t* torder) {
   const unsigned grid = (unsigned)((ntiles + kCountTiles - 1) / kCountTiles);
 #define CALL(KT, U, CZ)                                                                 \
   if (lut == 2)                                                                         \
     count_kernel<KT, U, 2, CZ><<<grid, kCountThreads, 0, st>>>(                          \
-        d, plan, tile_seg, hist, var_or, gt, ntiles, torder);                           \
+        d, plan, tile_seg, hist, var_or, var_and, gt, ntiles, torder);                           \
   else if (lut)                                                                         \
     count_kernel<KT, U, 1, CZ><<<grid, kCountThreads, 0, st>>>(                          \
-        d, plan, tile_seg, hist, var_or, gt, ntiles, torder);                           \
+        d, plan, tile_seg, hist, var_or, var_and, gt, ntiles, torder);                           \
   else                                                                                  \
     count_kernel<KT, U, 0, CZ><<<grid, kCountThreads, 0, st>>>(                          \
-        d, plan, tile_seg, hist, var_or, gt, ntiles, torder)
+        d, plan, tile_seg, hist, var_or, var_and, gt, ntiles, torder)
   SRS_KEY_DISPATCH(key_size, CALL)
 #undef CALL
 }
