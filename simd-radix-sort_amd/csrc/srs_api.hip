@@ -624,6 +624,7 @@ struct TablePlan {
 
 void plan_table(const std::vector<uint32_t>& h, int64_t n, int key_bits, TablePlan* P) {
   *P = TablePlan();
+
   // (host time here is GPU idle time: every pass below looks only at the
   // non-empty bins or is a plain integer sweep)
   std::vector<uint64_t> ct(512, 0);
@@ -655,13 +656,12 @@ void plan_table(const std::vector<uint32_t>& h, int64_t n, int key_bits, TablePl
     // a group's bins are one run of the (monotone) table
     std::vector<int32_t> fst(kGroups, -1), lst(kGroups, -1), nz0(kGroups, 0), nz1(kGroups, 0);
     std::vector<uint64_t> cnt(kGroups, 0);
-    fst[L[0]] = 0;
-    for (int b = 1; b < 65536; b++)
-      if (L[b] != L[b - 1]) {
-        lst[L[b - 1]] = b - 1;
-        fst[L[b]] = b;
-      }
-    lst[L[65535]] = 65535;
+    for (int g = 0; g < kGroups; g++) {  // (binary searches: L is monotone)
+      const auto a = std::lower_bound(L.begin(), L.end(), g);
+      if (a == L.end() || *a != g) continue;
+      fst[g] = (int32_t)(a - L.begin());
+      lst[g] = (int32_t)(std::upper_bound(a, L.end(), g) - L.begin()) - 1;
+    }
     for (size_t i = 0; i < nz.size(); i++) {  // the group's non-empty bins: nz[nz0, nz1)
       const int g = L[nz[i]];
       if (!cnt[g]) nz0[g] = (int32_t)i;
@@ -682,8 +682,9 @@ void plan_table(const std::vector<uint32_t>& h, int64_t n, int key_bits, TablePl
       const int bits = choose_bits((int64_t)len, key_bits - (16 - bl));
       if (bits >= bl) {  // each bin splits into 2^(bits - bl) buckets
         const double lim = (double)kLocalCap * (double)(1 << (bits - bl)) / to_n;
+        const double lim3 = lim + 3.0 * std::sqrt(lim);  // (sample noise)
         for (int i = nz0[g]; i < nz1[g]; i++)
-          if ((double)h[nz[i]] > lim) over += h[nz[i]] * to_n;
+          if ((double)h[nz[i]] > lim3) over += h[nz[i]] * to_n;
       } else {  // each bucket spans 2^(bl - bits) bins of the aligned range
         const int sh = bl - bits, b0 = fst[g] & ~((1 << bl) - 1);
         int qlo = kMaxBins, qhi = -1;
@@ -693,112 +694,121 @@ void plan_table(const std::vector<uint32_t>& h, int64_t n, int key_bits, TablePl
           qlo = std::min(qlo, q);
           qhi = std::max(qhi, q);
         }
+        const double lim = (double)kLocalCap / to_n, lim3 = lim + 3.0 * std::sqrt(lim);
         for (int q = qlo; q <= qhi; q++) {
-          if (qsum[q] * to_n > kLocalCap) over += qsum[q] * to_n;
+          if (qsum[q] > lim3) over += qsum[q] * to_n;
           qsum[q] = 0;
         }
       }
     }
     return over;
   };
+  // The 16-bit-table candidates (DigitLut mode 1, below) are planned only
+  // when the split table's predicted overflow is not already zero (they cost
+  // ~0.3 ms of host time, during which the GPU waits).
   std::vector<int32_t> lut(65536), first(kGroups, -1), last(kGroups, -1), rbits(kGroups);
-  {  // (an empty bin takes the group before it)
-    double before = 0;
-    int g = 0, at = 0;
-    for (int b : nz) {
-      std::fill(lut.begin() + at, lut.begin() + b, g);
-      const int x = (int)((before + 0.5 * h[b]) * kGroups / (double)total);
-      g = std::min(std::max(x, g), kGroups - 1);
-      lut[b] = g;
-      at = b + 1;
-      before += h[b];
-    }
-    std::fill(lut.begin() + at, lut.end(), g);
-  }
-  double over_best = overflow(lut);
-  {
-    std::vector<int32_t> la(65536, 0);
-    std::vector<double> x(512);
-    for (int t = 0; t < 512; t++) x[t] = (double)kGroups * (double)ct[t] / (double)total;
-    for (double sc = 1.0; sc > 0.5; sc -= 0.005) {
-      std::vector<int> nt(512, 0);
-      int S = 0;
-      double acc = 0;
-      bool open = false;
-      for (int t = 0; t < 512; t++) {
-        if (!ct[t]) continue;
-        if (x[t] < 1.0) {
-          if (!open || acc + x[t] > 1.0) {
-            S++;
-            open = true;
-            acc = 0;
-          }
-          acc += x[t];
-          continue;
-        }
-        open = false;
-        nt[t] = std::min(128, std::max(1, (int)std::lround(x[t] * sc)));
-        S += nt[t];
-      }
-      if (S > kGroups) continue;
-      int g = -1;
-      acc = 0;
-      open = false;
-      for (int t = 0; t < 512; t++) {
-        if (!ct[t] || x[t] < 1.0) {
-          if (ct[t] && (!open || acc + x[t] > 1.0)) {
-            g++;
-            open = true;
-            acc = 0;
-          }
-          acc += x[t];
-          for (int j = 0; j < 128; j++) la[t * 128 + j] = std::max(g, 0);
-          continue;
-        }
-        open = false;
-        const int base = g + 1;
-        double before = 0;
-        int prev = 0;
-        for (int j = 0; j < 128; j++) {
-          const double hj = h[t * 128 + j];
-          int k = (int)((before + 0.5 * hj) * nt[t] / (double)ct[t]);
-          k = std::min(std::max(k, prev), nt[t] - 1);
-          prev = k;
-          la[t * 128 + j] = base + k;
-          before += hj;
-        }
-        g = base + nt[t] - 1;
-      }
-      const double o = overflow(la);
-      if (o <= over_best) {
-        over_best = o;
-        lut.swap(la);
-      }
-      break;
-    }
-  }
-  for (int b = 0; b < 65536; b++) {
-    const int g = lut[b];
-    if (first[g] < 0) first[g] = b;
-    last[g] = b;
-  }
-  // the table only pays when its groups outnumber the plain digit's
-  // non-empty buckets (Gaussian int64 keys fill two 16-bit bins: both ways
-  // give two buckets, and the table pass is the slower one)
-  int groups_used = 0, buckets_used = 0;
-  {
-    std::vector<uint8_t> has(kGroups, 0);
-    for (int b : nz) has[lut[b]] = 1;
-    for (int g = 0; g < kGroups; g++) groups_used += has[g];
-  }
+  double over_best = -1;  // (-1: not evaluated)
+  int buckets_used = 0, groups_used = 0;
   for (int t = 0; t < 512; t++) buckets_used += ct[t] != 0;
-  if (groups_used < 2 * buckets_used) return;
-  for (int g = 0; g < kGroups; g++) {
-    const int diff = first[g] < 0 ? 0xFFFF : (first[g] ^ last[g]);
-    int bl = 0;
-    while ((1 << bl) <= diff) bl++;
-    rbits[g] = key_bits - (16 - bl);  // the group's keys share 16 - bl top bits
-  }
+  // false: no table pays
+  auto plan_mode1 = [&]() -> bool {
+    {  // (an empty bin takes the group before it)
+      double before = 0;
+      int g = 0, at = 0;
+      for (int b : nz) {
+        std::fill(lut.begin() + at, lut.begin() + b, g);
+        const int x = (int)((before + 0.5 * h[b]) * kGroups / (double)total);
+        g = std::min(std::max(x, g), kGroups - 1);
+        lut[b] = g;
+        at = b + 1;
+        before += h[b];
+      }
+      std::fill(lut.begin() + at, lut.end(), g);
+    }
+    over_best = overflow(lut);
+    {
+      std::vector<int32_t> la(65536, 0);
+      std::vector<double> x(512);
+      for (int t = 0; t < 512; t++) x[t] = (double)kGroups * (double)ct[t] / (double)total;
+      for (double sc = 1.0; sc > 0.5; sc -= 0.005) {
+        std::vector<int> nt(512, 0);
+        int S = 0;
+        double acc = 0;
+        bool open = false;
+        for (int t = 0; t < 512; t++) {
+          if (!ct[t]) continue;
+          if (x[t] < 1.0) {
+            if (!open || acc + x[t] > 1.0) {
+              S++;
+              open = true;
+              acc = 0;
+            }
+            acc += x[t];
+            continue;
+          }
+          open = false;
+          nt[t] = std::min(128, std::max(1, (int)std::lround(x[t] * sc)));
+          S += nt[t];
+        }
+        if (S > kGroups) continue;
+        int g = -1;
+        acc = 0;
+        open = false;
+        for (int t = 0; t < 512; t++) {
+          if (!ct[t] || x[t] < 1.0) {
+            if (ct[t] && (!open || acc + x[t] > 1.0)) {
+              g++;
+              open = true;
+              acc = 0;
+            }
+            acc += x[t];
+            for (int j = 0; j < 128; j++) la[t * 128 + j] = std::max(g, 0);
+            continue;
+          }
+          open = false;
+          const int base = g + 1;
+          double before = 0;
+          int prev = 0;
+          for (int j = 0; j < 128; j++) {
+            const double hj = h[t * 128 + j];
+            int k = (int)((before + 0.5 * hj) * nt[t] / (double)ct[t]);
+            k = std::min(std::max(k, prev), nt[t] - 1);
+            prev = k;
+            la[t * 128 + j] = base + k;
+            before += hj;
+          }
+          g = base + nt[t] - 1;
+        }
+        const double o = overflow(la);
+        if (o <= over_best) {
+          over_best = o;
+          lut.swap(la);
+        }
+        break;
+      }
+    }
+    for (int b = 0; b < 65536; b++) {
+      const int g = lut[b];
+      if (first[g] < 0) first[g] = b;
+      last[g] = b;
+    }
+    // the table only pays when its groups outnumber the plain digit's
+    // non-empty buckets (Gaussian int64 keys fill two 16-bit bins: both ways
+    // give two buckets, and the table pass is the slower one)
+    {
+      std::vector<uint8_t> has(kGroups, 0);
+      for (int b : nz) has[lut[b]] = 1;
+      for (int g = 0; g < kGroups; g++) groups_used += has[g];
+    }
+    if (groups_used < 2 * buckets_used) return false;
+    for (int g = 0; g < kGroups; g++) {
+      const int diff = first[g] < 0 ? 0xFFFF : (first[g] ^ last[g]);
+      int bl = 0;
+      while ((1 << bl) <= diff) bl++;
+      rbits[g] = key_bits - (16 - bl);  // the group's keys share 16 - bl top bits
+    }
+    return true;
+  };
   // Split table (DigitLut mode 3), when its next level overflows no more:
   // each top-9-bit bin t gets 2^lg_t consecutive groups, the next lg_t key
   // bits (no group spans two bins unless both are worth less than a group).
@@ -917,7 +927,11 @@ void plan_table(const std::vector<uint32_t>& h, int64_t n, int key_bits, TablePl
     }
     const double over3 = repr ? overflow(l3) : 1e300;
     const char* force = getenv("SRS_TABLE");  // (A/B runs: "1" or "3" forces the table kind)
-    const bool take3 = force && *force ? (*force == '3' && repr) : (repr && over3 <= over_best);
+    const bool forced = force && *force;
+    const bool early = !forced && repr && over3 == 0 &&
+                       S - (own ? empty_runs : 0) >= 2 * buckets_used;
+    if (!early && !plan_mode1()) return;
+    const bool take3 = forced ? (*force == '3' && repr) : (early || (repr && over3 <= over_best));
     if (take3) {
       // entry t: first group (bits 0..15) | lg (16..23); shared and empty
       // bins: the group (lg 0)

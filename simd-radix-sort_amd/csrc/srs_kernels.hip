@@ -934,8 +934,8 @@ __device__ __forceinline__ void count_flush(const SegPlan* __restrict__ plan, co
 // waves per SIMD the compiler must keep: 8 for the small-table passes of
 // keys up to 4 bytes (C2's first level lands at 7 otherwise), no constraint
 // elsewhere (forcing 8 on C1's plain pass spills 24 SGPRs it does not need
-// to; on the 8-byte range level it spills 30-54 VGPRs to scratch: that one
-// runs at 7 waves)
+// to; on the 8-byte range level it spills VGPRs to scratch even at 7: that
+// one runs at 6 waves, 73 VGPRs)
 template <int LUT, int KB>
 constexpr int kCountMinWaves = LUT == 2 && KB <= 4 ? 8 : 1;
 template <typename KT, typename U, int LUT, bool CZ>

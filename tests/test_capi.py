@@ -126,7 +126,7 @@ def test_hot_kernels_keep_their_occupancy():
                 occ = 6  # passes with the big digit table stage up to 26 KB in LDS
                 #          (the small-table kind, Li2E, keeps 8 waves per SIMD)
             if key == "count_kernel" and "ImmLi2E" in name:
-                occ = 7  # the 8-byte range level: 8 waves would spill VGPRs to scratch
+                occ = 6  # the 8-byte range level: 7 or 8 waves spill VGPRs to scratch
             assert r["Occupancy"] >= occ, (name, r)
     assert seen == set(need)
 
