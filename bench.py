@@ -440,11 +440,27 @@ def measure(cfg_name, args, torch, srs_amd, dist, dev, rank, world, shard):
             dist.barrier()
         torch.cuda.synchronize()
 
+    def collect():
+        out = {}
+        for name in ("count", "scatter", "local", "local_fast", "local_stable", "local_lsd",
+                     "scan", "plan", "children", "copy", "partition", "key_hist",
+                     *[f"{k}.L{i}" for i in range(1, 7) for k in ("count", "scatter")]):
+            try:
+                l, ms, el = srs_amd.kernel_stats(name)
+            except Exception:
+                continue
+            if l:
+                out[name] = {"launches": l, "ms": ms, "elems": el}
+        return out
+
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
     srs_amd.reset_kernel_stats()
-    srs_amd.set_kernel_timing(True)
+    # The timed steps carry HIP event markers around the scatter launches
+    # only (async stream packets, no host waits): the roofline's launch
+    # durations come from them.
+    srs_amd.set_kernel_timing(2)
     sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
@@ -453,25 +469,27 @@ def measure(cfg_name, args, torch, srs_amd, dist, dev, rank, world, shard):
     t1 = time.perf_counter()
     srs_amd.set_kernel_timing(False)
     elapsed = t1 - t0
-    # The timed steps carry HIP event markers around each launch (async
-    # stream packets, no host waits; the roofline's launch durations come
-    # from them). The same steps without the markers, for comparison:
-    kstats = {}
-    for name in ("count", "scatter", "local", "local_fast", "local_stable", "local_lsd", "scan",
-                 "plan", "children", "copy", "partition", "key_hist",
-                 *[f"{k}.L{i}" for i in range(1, 7) for k in ("count", "scatter")]):
-        try:
-            l, ms, el = srs_amd.kernel_stats(name)
-        except Exception:
-            continue
-        if l:
-            kstats[name] = {"launches": l, "ms": ms, "elems": el}
+    timed = collect()
+    # The per-kernel breakdown comes from a few more steps with markers
+    # around every launch (they cost a step 0.05-0.2 ms), and the same
+    # steps without any markers are timed for comparison.
+    nb = min(args.steps, 3)
+    srs_amd.reset_kernel_stats()
+    srs_amd.set_kernel_timing(True)
     sync()
     t2 = time.perf_counter()
-    for _ in range(min(args.steps, 3)):
+    for _ in range(nb):
         step()
     sync()
-    ms_no_events = (time.perf_counter() - t2) / min(args.steps, 3) * 1e3
+    ms_all_events = (time.perf_counter() - t2) / nb * 1e3
+    srs_amd.set_kernel_timing(False)
+    kstats = collect()
+    sync()
+    t2 = time.perf_counter()
+    for _ in range(nb):
+        step()
+    sync()
+    ms_no_events = (time.perf_counter() - t2) / nb * 1e3
     phases = None
     if shard:
         # per-rank phase stamps of the last step (HIP events), the bytes each
@@ -497,7 +515,8 @@ def measure(cfg_name, args, torch, srs_amd, dist, dev, rank, world, shard):
     dom = max((k for k in kstats if k in per_elem), key=lambda k: kstats[k]["ms"], default=None)
     roofline = None
     if dom:
-        s = kstats[dom]
+        # (the timed region's own durations when it measured this kernel)
+        s = timed[dom] if dom in timed else kstats[dom]
         avg_ms = s["ms"] / s["launches"]
         bytes_per_launch = per_elem[dom] * s["elems"] / s["launches"]
         achieved = bytes_per_launch / (avg_ms * 1e-3) / 1e9
@@ -514,7 +533,7 @@ def measure(cfg_name, args, torch, srs_amd, dist, dev, rank, world, shard):
     L_g = min(math.ceil(math.log(max(n / 4096, 1.0001), 256)), ks)
     b_alg = n * (L_g * (c_b + 2 * s_b) + 2 * s_b)
     pass_model_gbs = b_alg * world / (elapsed / args.steps) / 1e9
-    levels_run = (kstats.get("count", {}).get("launches", 0) / args.steps) if not shard else None
+    levels_run = (kstats.get("count", {}).get("launches", 0) / nb) if not shard else None
     pass_model = {"B_alg_bytes_per_gpu": b_alg, "L_g": L_g, "gbs": round(pass_model_gbs, 1),
                   "frac_of_8TBs": round(pass_model_gbs / world / HBM_PEAK_GBS, 4)}
     if levels_run:
@@ -542,6 +561,7 @@ def measure(cfg_name, args, torch, srs_amd, dist, dev, rank, world, shard):
         "unit": "Gkeys/s",
         "ms_per_step": round(ms_per_step, 3),
         "ms_per_step_without_event_markers": round(ms_no_events, 3),
+        "ms_per_step_with_all_event_markers": round(ms_all_events, 3),
         "dtype": kname if kname != "u64" else "uint64",
         "config": {"workload": cfg_name + ": " + cdesc +
                    ("" if args.dist == "uniform" or cfg_name != args.config
@@ -553,7 +573,7 @@ def measure(cfg_name, args, torch, srs_amd, dist, dev, rank, world, shard):
         "roofline": roofline,
         "pass_model": pass_model,
         "kernels": {k: {"launches": v["launches"], "avg_ms": round(v["ms"] / v["launches"], 4),
-                        "total_ms_per_step": round(v["ms"] / args.steps, 3)}
+                        "total_ms_per_step": round(v["ms"] / nb, 3)}
                     for k, v in kstats.items()},
         "verified": verified,
         **({"phases": phases} if phases is not None else {}),

@@ -276,7 +276,8 @@ const char* srs_last_error(void);
 const char* srs_version(void);
 
 /* Per-kernel timing with HIP events recorded on the launch stream around
- * every kernel launch (off by default). srs_kernel_stats fills, for kernel
+ * every kernel launch (enable 1; off by default; 2: around the scatter
+ * launches only, as bench.py's timed region). srs_kernel_stats fills, for kernel
  * name `name` ("count", "scatter", "local", "scan", ...), the number of
  * launches and the summed device milliseconds since the last reset; the
  * stream must have completed. Returns SRS_ERR_INVALID_ARG for unknown names. */

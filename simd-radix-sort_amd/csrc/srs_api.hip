@@ -16,6 +16,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <cstring>
 #include <cstdio>
 #include <cstdlib>
 #include <map>
@@ -128,7 +129,13 @@ struct KStat {
   double elems = 0;
 };
 std::mutex g_tmu;
-bool g_timing = false;
+// 0 off, 1 every launch scope, 2 only the scatter's (bench.py's timed
+// region: the roofline needs the dominant kernel's durations, and markers
+// around every launch cost the step 0.05-0.2 ms)
+int g_timing = 0;
+bool timing_wants(const char* name) {
+  return g_timing == 1 || (g_timing == 2 && strcmp(name, "scatter") == 0);
+}
 std::vector<TimingRec> g_pending;
 std::vector<hipEvent_t> g_event_pool;
 std::map<std::string, KStat> g_stats;
@@ -150,7 +157,7 @@ struct TimedScope {
   hipStream_t st;
   TimedScope(const char* name, double elems, hipStream_t s, int level = 0) : st(s) {
     std::lock_guard<std::mutex> lk(g_tmu);
-    if (!g_timing) return;
+    if (!timing_wants(name)) return;
     rec.name = name;
     if (level > 0) rec.name2 = std::string(name) + ".L" + std::to_string(level);
     rec.elems = elems;
@@ -168,12 +175,12 @@ struct TimedScope {
 
 bool timing_enabled() {
   std::lock_guard<std::mutex> lk(g_tmu);
-  return g_timing;
+  return g_timing != 0;
 }
 
 void note_elems(const char* name, double elems, int level = 0) {
   std::lock_guard<std::mutex> lk(g_tmu);
-  if (!g_timing) return;
+  if (!timing_wants(name)) return;
   g_stats[name].elems += elems;
   if (level > 0) g_stats[std::string(name) + ".L" + std::to_string(level)].elems += elems;
 }
@@ -2678,7 +2685,7 @@ int srs_set_host_devices(int32_t num_devices, const int32_t* devices) {
 
 int srs_set_kernel_timing(int enable) {
   std::lock_guard<std::mutex> lk(g_tmu);
-  g_timing = enable != 0;
+  g_timing = enable == 2 ? 2 : enable != 0;
   return SRS_OK;
 }
 

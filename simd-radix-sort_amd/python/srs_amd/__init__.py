@@ -356,8 +356,10 @@ def partition_device(keys, payloads, bits: int, part_of_bucket, num_parts: int, 
 # --------------------------------------------------------------------------
 # kernel timing (HIP events around every launch, see srs_c_api.h)
 # --------------------------------------------------------------------------
-def set_kernel_timing(enable: bool) -> None:
-    _check(lib().srs_set_kernel_timing(int(bool(enable))))
+def set_kernel_timing(enable) -> None:
+    """True / 1: HIP events around every launch; 2: around the scatter
+    launches only (the timed region's roofline kernel); False / 0: off."""
+    _check(lib().srs_set_kernel_timing(2 if enable == 2 else int(bool(enable))))
 
 
 def reset_kernel_stats() -> None:
