@@ -357,6 +357,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": res["ms_per_step"],
             "ms_per_step_without_event_markers": res["ms_per_step_without_event_markers"],
+            "ms_per_step_with_all_event_markers": res["ms_per_step_with_all_event_markers"],
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
@@ -473,7 +474,7 @@ def measure(cfg_name, args, torch, srs_amd, dist, dev, rank, world, shard):
     # The per-kernel breakdown comes from a few more steps with markers
     # around every launch (they cost a step 0.05-0.2 ms), and the same
     # steps without any markers are timed for comparison.
-    nb = min(args.steps, 3)
+    nb = min(args.steps, 5)
     srs_amd.reset_kernel_stats()
     srs_amd.set_kernel_timing(True)
     sync()
