@@ -1026,14 +1026,14 @@ int plan_balanced_level(Workspace* W, const Request& R, const SortDesc& d, bool*
   if (total == 0) return SRS_OK;
   if (!R.aos) {
     std::vector<KeyCluster> cl;
-    for (int b = 0; b < 65536; b++) {
+    bool ok = true;
+    for (int b = 0; b < 65536 && ok; b++) {  // (stops at the first cluster too many or too wide)
       if (!h[b]) continue;
       if (cl.empty() || b - cl.back().b1 > kClusterGap) cl.push_back(KeyCluster{b, b, 0});
       cl.back().b1 = b;
       cl.back().cnt += h[b];
+      ok = (int)cl.size() <= kMaxRanges && cl.back().b1 - cl.back().b0 < kClusterSpan;
     }
-    bool ok = (int)cl.size() <= kMaxRanges;
-    for (const KeyCluster& c : cl) ok &= c.b1 - c.b0 < kClusterSpan;
     if (ok) {
       *clusters = cl;
       return SRS_OK;

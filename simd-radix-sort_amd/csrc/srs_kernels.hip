@@ -951,9 +951,7 @@ __global__ __launch_bounds__(kCountThreads, (kCountMinWaves<LUT, (int)sizeof(KT)
   int64_t t0 = xcd_remap(blockIdx.x, gridDim.x) * kCountTiles;
   // gathered level: tiles in stripe order (each stripe's pieces lie back to
   // back, so the reads sweep memory); the rows do not depend on the order
-#ifndef SRS_DIAG_COUNT_NOTORDER
   if (torder && kCountTiles == 1) t0 = torder[t0];
-#endif
   __shared__ alignas(16) uint16_t slut[kLutLdsEntries<LUT>];
   U ra[kCountItems], rb[kCountItems];
   CountTile A = count_load<KT, U>(desc, plan, tile_seg, gt, t0, ntiles, ra);
