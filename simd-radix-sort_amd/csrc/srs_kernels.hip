@@ -42,7 +42,11 @@ __device__ __forceinline__ T gld(const void* p) {
 }
 template <typename T>
 __device__ __forceinline__ void gst(void* p, T v) {
+#if SRS_DIAG_NT_STORES  // (diagnostic: nontemporal element stores)
+  __builtin_nontemporal_store(v, (SRS_GLOBAL T*)(p));
+#else
   *(SRS_GLOBAL T*)(p) = v;
+#endif
 }
 
 __device__ __forceinline__ uint64_t load_w(const char* p, uint32_t w) {
