@@ -632,16 +632,22 @@ struct TablePlan {
 void plan_table(const std::vector<uint32_t>& h, int64_t n, int key_bits, TablePlan* P) {
   *P = TablePlan();
 
+
   // (host time here is GPU idle time: every pass below looks only at the
   // non-empty bins or is a plain integer sweep)
   std::vector<uint64_t> ct(512, 0);
   std::vector<int32_t> nz;  // the non-empty bins
   nz.reserve(8192);
-  for (int b = 0; b < 65536; b++)
-    if (h[b]) {
-      nz.push_back(b);
-      ct[b >> 7] += h[b];
-    }
+  for (int b0 = 0; b0 < 65536; b0 += 16) {  // (skips empty runs 16 bins at a time)
+    uint64_t any = 0;
+    for (int j = 0; j < 16; j++) any |= h[b0 + j];
+    if (!any) continue;
+    for (int b = b0; b < b0 + 16; b++)
+      if (h[b]) {
+        nz.push_back(b);
+        ct[b >> 7] += h[b];
+      }
+  }
   uint64_t total = 0;
   for (uint64_t c : ct) total += c;
   if (total == 0) return;
@@ -663,11 +669,21 @@ void plan_table(const std::vector<uint32_t>& h, int64_t n, int key_bits, TablePl
     // a group's bins are one run of the (monotone) table
     std::vector<int32_t> fst(kGroups, -1), lst(kGroups, -1), nz0(kGroups, 0), nz1(kGroups, 0);
     std::vector<uint64_t> cnt(kGroups, 0);
-    for (int g = 0; g < kGroups; g++) {  // (binary searches: L is monotone)
-      const auto a = std::lower_bound(L.begin(), L.end(), g);
-      if (a == L.end() || *a != g) continue;
-      fst[g] = (int32_t)(a - L.begin());
-      lst[g] = (int32_t)(std::upper_bound(a, L.end(), g) - L.begin()) - 1;
+    // each group's run of the (monotone) table: one forward sweep that
+    // gallops over each run instead of stepping through 65,536 entries
+    for (int b = 0; b < 65536;) {
+      const int g = L[b];
+      int step = 1;
+      while (b + step < 65536 && L[b + step] == g) step <<= 1;
+      int lo = b + (step >> 1), hi = std::min(b + step, 65536);  // last g in [lo, hi)
+      while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (L[mid] == g) lo = mid;
+        else hi = mid;
+      }
+      fst[g] = b;
+      lst[g] = lo;
+      b = lo + 1;
     }
     for (size_t i = 0; i < nz.size(); i++) {  // the group's non-empty bins: nz[nz0, nz1)
       const int g = L[nz[i]];
