@@ -264,10 +264,10 @@ __host__ __device__ inline int levels_for(int64_t len, int64_t target, int* need
 }
 
 // average bucket up to which a segment still takes one level fewer: its
-// buckets then land in the large LDS class (<= kLocalCap records, ~2.5x the
-// small class's cost per key) instead of paying a count + scatter level and
-// its launches and host sync (C2's few oversized first-level groups: a
-// third and fourth level on ~1 % of the keys)
+// buckets then land in the large LDS class (<= kLocalCap records; its own
+// direct kernel since round 4) instead of paying a count + scatter level and
+// its launches and host sync. 512 x 7808 = 4.0 M: C2's densest first-level
+// groups hold 3.9 M keys
 constexpr int kLocalCapTarget = 7808;
 
 __host__ __device__ inline int choose_bits(int64_t len, int rbits) {
