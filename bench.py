@@ -11,8 +11,9 @@ and are resident in HBM before the timed region.
 
 N > 1 (torchrun, one rank per GPU): every rank holds 1e9 keys (indices
 [r*1e9, (r+1)*1e9)); the global array is sorted across ranks by the
-top-radix-bits shard: histogram all-reduce, partition,
-all-to-all over RCCL, local sort. Weak scaling.
+top-radix-bits shard of the library's C ABI (srs_shard_*,
+csrc/srs_shard.hip, through ctypes): histogram all-reduce, partition,
+grouped send/recv over RCCL/xGMI, local sort. Weak scaling.
 
 Prints ONE JSON line on rank 0.
 """
@@ -53,13 +54,21 @@ def parse():
     ap.add_argument("--cpu-sample", type=float, default=1e9,
                     help="keys of the headline config's CPU baseline (the reference on one "
                          "host core; 1e9 = the config itself; 0 = skip)")
-    ap.add_argument("--cpu-sample-extra", type=float, default=2 ** 27,
-                    help="keys of the CPU-baseline sample of each 'extra' config (0 = skip)")
+    ap.add_argument("--cpu-sample-extra", type=float, default=1e9,
+                    help="keys of the CPU-baseline sample of each 'extra' config (1e9 = the "
+                         "config itself; 0 = skip)")
     ap.add_argument("--cpu-warmup", type=int, default=1,
                     help="untimed warmup sorts before the timed CPU-baseline sort")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--shard", action="store_true",
                     help="run the multi-GPU shard protocol even at one rank (RCCL, world 1)")
+    ap.add_argument("--rounds", type=int, default=0,
+                    help="shard exchange rounds (srs_shard_set_options; 0 = library default)")
+    ap.add_argument("--chunks", type=int, default=0,
+                    help="shard partition chunks (srs_shard_set_options; 0 = library default)")
+    ap.add_argument("--alloc-steps", type=int, default=3,
+                    help="world 1: extra steps with outputs from torch's allocator and in place "
+                         "on a torch array (ms_per_step_plain_alloc / _inplace; 0 = skip)")
     ap.add_argument("--extra", default="c2,c3",
                     help="comma list of further configs measured after the headline one and "
                          "reported under 'extra' (world 1, c1 headline only; 'none' = skip)")
@@ -358,6 +367,8 @@ def main():
             "ms_per_step": res["ms_per_step"],
             "ms_per_step_without_event_markers": res["ms_per_step_without_event_markers"],
             "ms_per_step_with_all_event_markers": res["ms_per_step_with_all_event_markers"],
+            **{k: res[k] for k in ("ms_per_step_plain_alloc", "ms_per_step_inplace",
+                                   "alloc_variants") if k in res},
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
@@ -421,13 +432,20 @@ def measure(cfg_name, args, torch, srs_amd, dist, dev, rank, world, shard):
     if shard:
         if layout != "soa":
             raise SystemExit("multi-GPU bench runs the SoA configs (c1, c2)")
-        from srs_amd.dist import HipShardOps, ShardSorter  # multi-GPU path (RCCL)
-        sorter = ShardSorter(HipShardOps(kind), n, [p.dtype for p in pays], keys.dtype, dev)
+        # the library's shard sort over RCCL (srs_shard_*): rank 0's unique
+        # id reaches every rank through torch.distributed
+        from srs_amd import shard as shard_mod
+        uid = torch.zeros(shard_mod.ID_BYTES, dtype=torch.uint8, device=dev)
+        if rank == 0:
+            uid.copy_(torch.frombuffer(bytearray(shard_mod.unique_id()), dtype=torch.uint8))
+        dist.broadcast(uid, 0)
+        comm = shard_mod.ShardComm.rccl(world, rank, bytes(uid.cpu().numpy().tobytes()), dev)
+        comm.set_options(args.rounds, args.chunks)
     shard_out = []
 
     def step():
         if shard:
-            shard_out[:] = [sorter.sort(keys, pays)]
+            shard_out[:] = [comm.sort(keys, *pays, key_kind=kind)]
             return
         if layout == "aos":
             srs_amd.sort_combined_device(rec, kind, out=rec_out, cmp_sorter=args.cmp_sorter)
@@ -556,6 +574,8 @@ def measure(cfg_name, args, torch, srs_amd, dist, dev, rank, world, shard):
     elif not args.no_verify:
         verified = verify_shards(keys, pays, shard_out[0], kname, psizes, torch, dist, dev)
     del keys, pays, keys_out, pays_out, rec, rec_out, shard_out
+    if shard:
+        comm.close()
 
     return {
         "value": round(gkeys, 4),
@@ -577,8 +597,59 @@ def measure(cfg_name, args, torch, srs_amd, dist, dev, rank, world, shard):
                         "total_ms_per_step": round(v["ms"] / nb, 3)}
                     for k, v in kstats.items()},
         "verified": verified,
+        **alloc_ms,
         **({"phases": phases} if phases is not None else {}),
     }
+
+
+def alloc_variants(args, step_args, torch, srs_amd):
+    """What a caller that does not use srs_alloc_device gets:
+    a few steps whose outputs come from torch's allocator (plain hipMalloc
+    memory) and a few steps sorting a torch array IN PLACE (the reference's
+    own contract, radixSort.hpp:1780), each on a fresh copy of the input
+    (the copy is outside the timed sort). Per-step times (synchronised), in
+    ms; the median is reported."""
+    keys, pays, rec, kind, layout = step_args
+    k = args.alloc_steps
+    src = [rec] if layout == "aos" else [keys, *pays]
+    outs = [torch.empty_like(t) for t in src]
+    work = [torch.empty_like(t) for t in src]
+
+    def sort(cols, out):
+        if layout == "aos":
+            srs_amd.sort_combined_device(cols[0], kind, out=None if out is None else out[0],
+                                         cmp_sorter=args.cmp_sorter)
+        else:
+            srs_amd.sort_device(cols[0], *cols[1:], key_kind=kind, out=out,
+                                cmp_sorter=args.cmp_sorter)
+
+    def timed(fn, prep=None):
+        ts = []
+        for _ in range(k):
+            if prep:
+                prep()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            fn()
+            torch.cuda.synchronize()
+            ts.append((time.perf_counter() - t0) * 1e3)
+        return round(sorted(ts)[len(ts) // 2], 3), [round(t, 3) for t in ts]
+
+    def restore():
+        for w, s_ in zip(work, src):
+            w.copy_(s_)
+    plain, plain_all = timed(lambda: sort(src, tuple(outs)))
+    inplace, inplace_all = timed(lambda: sort(work, None), prep=restore)
+    ok = all(torch.equal(w, o) for w, o in zip(work, outs))
+    del outs, work
+    torch.cuda.empty_cache()
+    return {"ms_per_step_plain_alloc": plain, "ms_per_step_inplace": inplace,
+            "alloc_variants": {"steps": k, "plain_alloc_ms": plain_all, "inplace_ms": inplace_all,
+                               "inplace_equals_out_of_place": ok,
+                               "note": "outputs from torch's allocator / sorted in place on a "
+                                       "torch array restored from the input before each step; "
+                                       "median of the steps (the headline's outputs come from "
+                                       "srs_alloc_device)"}}
 
 
 def _order_view(k, kname, torch):

@@ -190,19 +190,29 @@ int srs_partition_device(int64_t num, int key_kind, int up, const void* keys,
                          void* keys_out, void* const* payloads_out,
                          int64_t* part_counts, void* stream);
 
-/* ---- the multi-GPU shard sort over RCCL (C ABI) ------------
+/* ---- the multi-GPU shard sort (C ABI) ----------------------
  * One array spread over N GPUs is sorted across them: rank r ends with the
  * r-th key range, so concatenating the ranks' outputs gives the sorted array
  * (stable). The protocol is the one above: histogram all-reduce, 512
  * key-range groups, chunked partition, rounds of grouped send/recv over
- * xGMI, each round's range sorted on a side stream while the next is in
- * flight. RCCL is loaded at first use (librccl.so.1); without it these
- * return SRS_ERR_NO_DEVICE. The reference has no multi-device path.
+ * xGMI, each round's range sorted on a side stream while the later rounds
+ * are in flight. RCCL is loaded at first use (librccl.so.1); without it the
+ * RCCL communicators return SRS_ERR_NO_DEVICE. The reference has no
+ * multi-device path. This is the only implementation of the protocol (the
+ * Python bench drives it through ctypes).
  *
  * Communicators: one process per GPU (srs_shard_unique_id on one rank, the
  * 128 bytes passed to every rank, srs_shard_comm_init on each with its GPU
  * current), or one process driving several GPUs (srs_shard_comm_init_all,
- * then srs_shard_sort_multi). */
+ * then srs_shard_sort_multi).
+ *
+ * Failures: every rank returns an error if any rank fails (invalid or
+ * disagreeing arguments, an allocation, a partition or a round sort), with
+ * the communicator still usable afterwards; a rank never returns early while
+ * its peers wait for its messages. A transport failure (RCCL error, timeout)
+ * aborts the communicator (ncclCommAbort): later sorts on it fail and it
+ * must be destroyed. Host waits on peers are bounded by SRS_SHARD_TIMEOUT_S
+ * seconds (default 600). */
 #define SRS_SHARD_ID_BYTES 128
 typedef struct srs_shard_comm_s* srs_shard_comm;
 int srs_shard_unique_id(void* id);
@@ -210,23 +220,63 @@ int srs_shard_comm_init(int32_t world, int32_t rank, const void* id, srs_shard_c
 int srs_shard_comm_init_all(int32_t num_devices, const int32_t* devices, srs_shard_comm* comms);
 int srs_shard_comm_destroy(srs_shard_comm comm);
 
+/* `world` communicators over the CURRENT device whose collectives and peer
+ * messages travel through host memory (threads of one process; drive them
+ * with srs_shard_sort_multi). Every kernel of the protocol runs as with
+ * RCCL; only the transport differs. For tests and for machines with fewer
+ * GPUs than ranks (RCCL puts no two ranks on one device). */
+int srs_shard_comm_init_staged(int32_t world, srs_shard_comm* comms);
+
+/* Exchange rounds (1..64) and partition chunks (1..16) of later sorts on
+ * this communicator; 0 = the default (8 rounds; 8 chunks from 2 ranks up,
+ * 1 at one rank). Every rank must use the same values (checked: a mismatch
+ * fails every rank with SRS_ERR_INVALID_ARG). */
+int srs_shard_set_options(srs_shard_comm comm, int32_t rounds, int32_t chunks);
+
 /* This rank's part of the shard sort of device columns (inputs untouched):
  * *keys_out / payloads_out[k] receive device pointers to this rank's sorted
  * key range and *num_out its length; the memory belongs to the communicator
- * and stays valid until its next sort or its destruction. On `stream`; every
- * rank of the communicator must call it. */
+ * and stays valid until its next sort or its destruction. Work runs on
+ * `stream` (and the communicator's own streams); the call returns when the
+ * sort is complete. Every rank of the communicator must call it. */
 int srs_shard_sort_device(srs_shard_comm comm, int64_t num, int key_kind, int up,
                           const void* keys, int32_t num_payloads, const void* const* payloads,
                           const uint32_t* payload_sizes, void** keys_out, void** payloads_out,
                           int64_t* num_out, void* stream);
 
 /* All ranks of a single-process communicator set at once (one host thread
- * per GPU; synchronous): rank i sorts nums[i] records at keys[i] and
+ * per rank; synchronous): rank i sorts nums[i] records at keys[i] and
  * payloads[i * num_payloads + k]; outputs as above, per rank. */
 int srs_shard_sort_multi(int32_t num_devices, const srs_shard_comm* comms, const int64_t* nums,
                          int key_kind, int up, const void* const* keys, int32_t num_payloads,
                          const void* const* payloads, const uint32_t* payload_sizes,
                          void** keys_out, void** payloads_out, int64_t* nums_out);
+
+/* The last successful sort on this communicator as JSON: transport, world,
+ * rank, chunks, rounds, groups, records in / out, record bytes, "stamps_ms"
+ * (HIP-event times since its start of: hist, plan, partition<c>,
+ * round<r>_recv, round<r>_sort_start, round<r>_sort_end, end) and
+ * "bytes_to_peer_per_round" ([round][peer] bytes this rank sent). */
+int srs_shard_last_report(srs_shard_comm comm, char* buf, int64_t cap);
+
+/* Test hook: the next sort on this communicator fails at `point` (0 = none,
+ * 1 = argument error, 2 = allocation before the exchange, 3 = partition
+ * after the first messages, 4 = the last round's sort, 5 = transport
+ * failure after the first messages: aborts). */
+int srs_shard_debug_inject(srs_shard_comm comm, int32_t point);
+
+/* The shard plan of one rank, host only (no GPU): from every rank's chunk
+ * histograms (chunk_hists[src][chunk][2^min(12, key_bits)] of the
+ * transformed top key bits) and this rank's record count, the JSON of
+ * group_of_bin, rank_of_group, chunk_bounds, total (records received),
+ * "posts" (every message group in posting order: round, chunks, msgs =
+ * [op (0 send, 1 receive, 2 own-piece copy), peer, partitioned offset,
+ * receive offset, records]) and "rounds" (each round's receive range, its
+ * sort segments and known top bits). The same code plans the device sort;
+ * tests drive the protocol with it on CPU (gloo). */
+int srs_debug_shard_plan(int32_t world, int32_t rank, int32_t chunks, int32_t rounds,
+                         int32_t key_bits, const uint64_t* chunk_hists, int64_t num, char* json,
+                         int64_t cap);
 
 /* ---- host arrays over several GPUs --------------------------------------- */
 

@@ -347,7 +347,14 @@ hipError_t big_free(void* p, int mode) {
 // other memory), keeping the fastest. Small buffers are not probed.
 constexpr size_t kPlaceMinBytes = size_t(256) << 20;
 constexpr int kPlaceTries = 4;
-std::mutex g_plmu;
+// One placement at a time per device (probes of two buffers on one device
+// would time each other). Nothing here waits for other work on the device:
+// the probe runs on a private stream and touches only the new buffer, so a
+// thread that allocates while its device holds queued peer receives (the
+// multi-GPU shard, one host thread per GPU) never waits for another thread.
+std::mutex g_plmu_map;                       // the map below
+std::map<int, std::unique_ptr<std::mutex>> g_plmu;
+std::mutex g_place_ref_mu;
 double g_place_ref = 0;  // fastest probe seen, ms per GB (0: none yet)
 
 bool placement_enabled() {
@@ -355,14 +362,30 @@ bool placement_enabled() {
   return !(e && *e == '0');
 }
 
+std::mutex& device_place_mutex(int dev) {
+  std::lock_guard<std::mutex> g(g_plmu_map);
+  auto& m = g_plmu[dev];
+  if (!m) m.reset(new std::mutex());
+  return *m;
+}
+
 hipError_t placed_alloc(void** p, size_t bytes, int mode) {
   if (bytes < kPlaceMinBytes || !placement_enabled()) return big_alloc(p, bytes, mode);
-  std::lock_guard<std::mutex> g(g_plmu);
-  hipError_t e = hipDeviceSynchronize();  // (the probe runs on the null stream)
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  std::lock_guard<std::mutex> g(device_place_mutex(dev));
+  hipStream_t ps = nullptr;
+  e = hipStreamCreateWithFlags(&ps, hipStreamNonBlocking);
   if (e != hipSuccess) return e;
   void* best = nullptr;
   double best_rate = 0;
-  const double ref = g_place_ref;  // the fastest placement of earlier buffers
+  double ref = 0;  // the fastest placement of earlier buffers
+  {
+    std::lock_guard<std::mutex> r(g_place_ref_mu);
+    ref = g_place_ref;
+  }
+  double seen = ref;  // the fastest placement seen so far, this one included
   std::vector<void*> rejected;
   for (int k = 0; k < kPlaceTries; k++) {
     if (k > 0) {
@@ -373,11 +396,12 @@ hipError_t placed_alloc(void** p, size_t bytes, int mode) {
     e = big_alloc(&c, bytes, mode);
     if (e != hipSuccess) {
       if (best) break;  // (keep what we have)
+      (void)hipStreamDestroy(ps);
       return e;
     }
-    const float ms = probe_write_ms(c, bytes);
+    const float ms = probe_write_ms(c, bytes, ps);
     const double rate = ms > 0 ? ms / ((double)bytes / 1e9) : 0;  // ms per GB
-    if (rate > 0 && (g_place_ref == 0 || rate < g_place_ref)) g_place_ref = rate;
+    if (rate > 0 && (seen == 0 || rate < seen)) seen = rate;
     if (!best || (rate > 0 && rate < best_rate)) {
       if (best) rejected.push_back(best);
       best = c;
@@ -387,10 +411,15 @@ hipError_t placed_alloc(void** p, size_t bytes, int mode) {
     }
     if (best_rate <= 0) break;  // (no probe possible: keep it)
     if (ref > 0 ? best_rate <= 1.12 * ref
-                : k > 0 && best_rate <= 1.12 * g_place_ref)  // (first buffer: two looks)
+                : k > 0 && best_rate <= 1.12 * seen)  // (first buffer: two looks)
       break;
   }
+  {
+    std::lock_guard<std::mutex> r(g_place_ref_mu);
+    if (seen > 0 && (g_place_ref == 0 || seen < g_place_ref)) g_place_ref = seen;
+  }
   for (void* r : rejected) (void)big_free(r, mode);
+  (void)hipStreamDestroy(ps);
   (void)hipGetLastError();
   *p = best;
   return hipSuccess;
@@ -2477,6 +2506,22 @@ int set_leaf_mode(Request& R, int leaf_mode) {
 
 // (other translation units of the library report errors through this)
 int set_error(int code, const std::string& msg) { return fail(code, msg); }
+
+// Grows the current device's workspace so that a later
+// srs_sort_segments_device of up to `num` records of these column widths
+// allocates no large buffer: the multi-GPU shard reserves it before its first
+// message is posted, so that no rank can fail an allocation (or wait in one)
+// once its peers depend on it (srs_shard.hip).
+int reserve_segments_workspace(int64_t num, int ncols, const uint32_t* widths) {
+  size_t tmp_bytes = 0;
+  for (int c = 0; c < ncols; c++) tmp_bytes += align_up((size_t)std::max<int64_t>(num, 1) * widths[c], 256);
+  Workspace* W = nullptr;
+  WsLock lk;
+  SRS_TRY(acquire_ws(&W, &lk));
+  if (W->tmp.p && W->tmp.bytes >= tmp_bytes) return SRS_OK;
+  if (W->idle && W->idle_pending) HIP_TRY(hipEventSynchronize(W->idle));  // (the old TMP's last use)
+  return ensure(W->tmp, tmp_bytes, ws_alloc_mode(), true);
+}
 }  // namespace srs
 
 using namespace srs;
@@ -2861,7 +2906,10 @@ int srs_debug_free(void* ptr) {
 
 int srs_debug_probe_write(void* ptr, uint64_t bytes, float* ms) {
   if (!ptr || !ms) return fail(SRS_ERR_INVALID_ARG, "srs_debug_probe_write: ptr and ms");
-  *ms = probe_write_ms(ptr, (size_t)bytes);
+  hipStream_t ps = nullptr;
+  HIP_TRY(hipStreamCreateWithFlags(&ps, hipStreamNonBlocking));
+  *ms = probe_write_ms(ptr, (size_t)bytes, ps);
+  (void)hipStreamDestroy(ps);
   HIP_TRY(hipGetLastError());
   return SRS_OK;
 }

@@ -83,7 +83,7 @@ void launch_fill(int64_t n, int kind, uint64_t seed, uint64_t first, void* keys,
                  int npay, const Col* pays, hipStream_t st);
 void launch_set_desc(const SortDesc& d, SortDesc* out, hipStream_t st);
 // placement probe: ms of the scatter's write pattern over a buffer (sync)
-float probe_write_ms(void* buf, size_t bytes);
+float probe_write_ms(void* buf, size_t bytes, hipStream_t st);
 // diagnostics: phase of each XCD's walk over its block range (xcd_remap)
 void set_xcd_rotation(int mode);
 // the copy list (finished segments not in OUT) home in one launch, column by

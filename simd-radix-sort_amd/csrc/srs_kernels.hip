@@ -3578,8 +3578,8 @@ __global__ __launch_bounds__(256) void place_probe_kernel(char* __restrict__ buf
 }
 
 // Average milliseconds of one probe pass over [buf, buf + bytes) (2 passes
-// after one warmup; synchronous).
-float probe_write_ms(void* buf, size_t bytes) {
+// after one warmup, on stream st; synchronous on st only).
+float probe_write_ms(void* buf, size_t bytes, hipStream_t st) {
   const int64_t windows = (int64_t)(bytes / kProbeWindow);
   if (windows < 1) return 0.f;
   constexpr int64_t kTiles = kProbeWindow / 512 / 64 / 2;
@@ -3590,10 +3590,10 @@ float probe_write_ms(void* buf, size_t bytes) {
     (void)hipEventDestroy(a);
     return 0.f;
   }
-  place_probe_kernel<<<grid, 256>>>((char*)buf, windows);
-  (void)hipEventRecord(a, 0);
-  for (int k = 0; k < 2; k++) place_probe_kernel<<<grid, 256>>>((char*)buf, windows);
-  (void)hipEventRecord(b, 0);
+  place_probe_kernel<<<grid, 256, 0, st>>>((char*)buf, windows);
+  (void)hipEventRecord(a, st);
+  for (int k = 0; k < 2; k++) place_probe_kernel<<<grid, 256, 0, st>>>((char*)buf, windows);
+  (void)hipEventRecord(b, st);
   float ms = 0.f;
   if (hipEventSynchronize(b) != hipSuccess || hipEventElapsedTime(&ms, a, b) != hipSuccess) ms = 0.f;
   (void)hipEventDestroy(a);

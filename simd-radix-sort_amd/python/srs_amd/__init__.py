@@ -304,7 +304,7 @@ def fill_synthetic_device(keys, *payloads, seed: int = 42 << 32, first_index: in
 
 
 # --------------------------------------------------------------------------
-# multi-GPU shard primitives (see srs_amd.dist)
+# multi-GPU shard primitives (the shard sort itself: srs_amd.shard)
 # --------------------------------------------------------------------------
 def key_histogram_device(keys, hist, bits: int, up: bool = True, key_kind: int | None = None,
                          stream=None) -> None:

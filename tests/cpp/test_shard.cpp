@@ -1,4 +1,5 @@
-// test_shard.cpp — the multi-GPU shard sort through the C ABI over RCCL
+// test_shard.cpp — the multi-GPU shard sort through the C ABI (RCCL and the
+// host-staged transport)
 // (srs_shard_*), driven from C++ with no torch: the
 // single-process communicator (srs_shard_comm_init_all + srs_shard_sort_multi)
 // and the one-process-per-GPU one (srs_shard_unique_id + srs_shard_comm_init
@@ -116,6 +117,39 @@ int main(int argc, char** argv) {
   }
   CK(srs_shard_comm_destroy(c2));
   CK(hipStreamDestroy(st));
-  printf("shard ok: n=%lld, both communicators equal the one-GPU sort\n", (long long)n);
+
+  // 3. three ranks on this GPU over the host-staged transport: the input cut
+  // into three ragged shards; the concatenated outputs equal the sort
+  {
+    const int W = 3;
+    srs_shard_comm cs[W];
+    CK(srs_shard_comm_init_staged(W, cs));
+    const int64_t cut[W + 1] = {0, n / 7, n / 7 + n / 2, n};
+    int64_t nm[W];
+    const void* km[W];
+    const void* pm[W];
+    void* ko3[W];
+    void* po3[W];
+    int64_t no3[W];
+    for (int r = 0; r < W; r++) {
+      nm[r] = cut[r + 1] - cut[r];
+      km[r] = (const char*)keys + cut[r] * 8;
+      pm[r] = (const char*)pays + cut[r] * 8;
+    }
+    CK(srs_shard_sort_multi(W, cs, nm, SRS_KEY_U64, 1, km, 1, pm, psz, ko3, po3, no3));
+    int64_t at = 0;
+    for (int r = 0; r < W; r++) {
+      if (at + no3[r] > n) return 1;
+      CK(hipMemcpy(sk.data() + at, ko3[r], (size_t)no3[r] * 8, hipMemcpyDeviceToHost));
+      CK(hipMemcpy(sp.data() + at, po3[r], (size_t)no3[r] * 8, hipMemcpyDeviceToHost));
+      at += no3[r];
+    }
+    if (at != n || memcmp(sk.data(), rk.data(), bytes) || memcmp(sp.data(), rp.data(), bytes)) {
+      fprintf(stderr, "shard (staged, 3 ranks) differs from the one-GPU sort\n");
+      return 1;
+    }
+    for (int r = 0; r < W; r++) CK(srs_shard_comm_destroy(cs[r]));
+  }
+  printf("shard ok: n=%lld, every communicator kind equals the one-GPU sort\n", (long long)n);
   return 0;
 }

@@ -121,8 +121,7 @@ def test_dropin_rejects_what_the_reference_rejects(call, msg):
 
 @pytest.mark.gpu
 def test_dropin_matrix_on_gpu():
-    if not os.path.exists(BIN):
-        subprocess.run(["make", "-C", CPP], check=True)
+    subprocess.run(["make", "-C", CPP, "_build/test_dropin"], check=True)  # (incremental)
     r = subprocess.run([BIN, "10000", "42"], capture_output=True, text=True, timeout=900)
     tail = "\n".join(r.stdout.splitlines()[-12:])
     assert r.returncode == 0 and "All tests passed" in r.stdout, tail + r.stderr[-2000:]
@@ -130,9 +129,10 @@ def test_dropin_matrix_on_gpu():
 
 @pytest.mark.gpu
 def test_shard_sort_cabi_over_rccl_matches_reference(tmp_path):
-    """The multi-GPU shard sort through the C ABI over RCCL, driven from C++
-    without torch (tests/cpp/test_shard.cpp): both communicator kinds at
-    world 1 equal the one-GPU sort bit for bit, and (here) the output equals
+    """The multi-GPU shard sort through the C ABI, driven from C++ without
+    torch (tests/cpp/test_shard.cpp): both RCCL communicator kinds at world 1
+    and three ranks over the host-staged transport equal the one-GPU sort bit
+    for bit, and (here) the output equals
     the REFERENCE's own sort of the same input (oracle/_ref, radixSort.hpp)
     at 2^25 + 1234 records: the shard path's partition level, segmented
     round sorts and stripe/gathered levels all run."""
@@ -142,8 +142,7 @@ def test_shard_sort_cabi_over_rccl_matches_reference(tmp_path):
     if ref_lib() is None:
         pytest.fail("oracle/_ref/libsrs_ref.so missing or host lacks AVX-512 VBMI2")
     binp = os.path.join(CPP, "_build", "test_shard")
-    if not os.path.exists(binp):
-        subprocess.run(["make", "-C", CPP, "_build/test_shard"], check=True)
+    subprocess.run(["make", "-C", CPP, "_build/test_shard"], check=True)  # (incremental)
     n = (1 << 25) + 1234
     prefix = str(tmp_path / "shard")
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")

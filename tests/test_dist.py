@@ -1,8 +1,13 @@
-"""Multi-process tests of the top-radix-bits shard protocol (srs_amd.dist)
-on CPU with the gloo backend, world_size 2 and 3. The device kernels are
-replaced by a numpy backend that follows the same contracts (stable
-partition by a bucket -> rank table; stable sort in the reference key order);
-the GPU kernels themselves are covered by the -m gpu tests."""
+"""The multi-GPU shard protocol's plan on CPU: the library's own planner
+(srs_debug_shard_plan: the host code srs_shard.hip runs on every rank, no
+GPU needed) drives a gloo world of 2-4 processes. Each rank histograms and
+partitions its keys with numpy (stable, by the plan's bin -> group table),
+executes the plan's message groups in its posting order with gloo
+send/recv, sorts each round's segments with numpy after checking the top
+key bits the plan says they share, and the union must equal a stable sort of
+every rank's input in (rank, index) order. The device side of the same
+protocol (histogram, partition and round-sort kernels, both transports) runs
+in tests/test_shard_gpu.py. The reference has no multi-device path."""
 import os
 import socket
 import sys
@@ -15,6 +20,8 @@ import torch.multiprocessing as mp
 
 from srs_testlib import KIND_UINT, key_size, transformed_keys
 
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
 
 def _free_port():
     with socket.socket() as s:
@@ -22,61 +29,123 @@ def _free_port():
         return s.getsockname()[1]
 
 
-class NumpyShardOps:
-    """CPU stand-in for HipShardOps with the same contracts."""
-
-    def __init__(self, kind):
-        self.kind = kind
-
-    def _u(self, keys):
-        return transformed_keys(self.kind, True, keys.numpy())
-
-    def histogram(self, keys, bits):
-        top = self._u(keys) >> np.uint64(8 * key_size(self.kind) - bits)
-        return torch.from_numpy(np.bincount(top.astype(np.int64), minlength=1 << bits)
-                                .astype(np.int64))
-
-    def partition(self, keys, pays, bits, part_of_bucket, nparts, out):
-        top = (self._u(keys) >> np.uint64(8 * key_size(self.kind) - bits)).astype(np.int64)
-        dest = part_of_bucket.numpy()[top]
-        order = np.argsort(dest, kind="stable")
-        out[0][:len(order)] = keys[torch.from_numpy(order)]
-        for o, p in zip(out[1:], pays):
-            o[:len(order)] = p[torch.from_numpy(order)]
-        return np.bincount(dest, minlength=nparts).tolist()
-
-    def sort(self, keys, pays):
-        order = torch.from_numpy(np.argsort(self._u(keys), kind="stable"))
-        keys.copy_(keys[order])
-        for p in pays:
-            p.copy_(p[order])
-
-    def sort_segments(self, keys, pays, bounds, known_top_bits=0, stamp=None):
-        if stamp:
-            stamp("sort_start", None)
-        # the known prefix must really be shared inside every segment
-        for a, b in zip(bounds[:-1], bounds[1:]):
-            if b > a and known_top_bits:
-                top = self._u(keys[a:b]) >> np.uint64(8 * key_size(self.kind) - known_top_bits)
-                assert (top == top[0]).all()
-        for a, b in zip(bounds[:-1], bounds[1:]):
-            self.sort(keys[a:b], [p[a:b] for p in pays])
-        if stamp:
-            stamp("sort_end", None)
-
-    def finish(self, device):
-        pass
+def _shard():
+    sys.path.insert(0, os.path.join(REPO, "simd-radix-sort_amd", "python"))
+    from srs_amd import shard
+    return shard
 
 
-def _worker(rank, world, port, kind, n_per, dist_kind, q, bits=8, chunks=4):
+def _top(kind, keys, bits):
+    return (transformed_keys(kind, True, keys) >> np.uint64(8 * key_size(kind) - bits)).astype(
+        np.int64)
+
+
+def _chunk_hists(kind, keys, chunks, bits):
+    n = len(keys)
+    out = np.zeros((chunks, 1 << bits), np.uint64)
+    top = _top(kind, keys, bits)
+    for c in range(chunks):
+        a, b = n * c // chunks, n * (c + 1) // chunks
+        out[c] = np.bincount(top[a:b], minlength=1 << bits)
+    return out
+
+
+def _make_keys(kind, dist_kind, n, rng):
+    ut = KIND_UINT[kind]
+    kb = 8 * key_size(kind)
+    if dist_kind == "uniform":
+        return rng.integers(0, 2**63, n, dtype=np.uint64).astype(ut)
+    if dist_kind == "skewed":  # a few top buckets + duplicates
+        return (rng.integers(0, 3, n, dtype=np.uint64) << np.uint64(kb - 3)
+                | rng.integers(0, 1000, n, dtype=np.uint64)).astype(ut)
+    return np.full(n, 7, dtype=ut)  # all equal
+
+
+def _run_rank(rank, world, kind, dist_kind, n_per, chunks, rounds):
+    shard = _shard()
+    rng = np.random.default_rng(100 + rank)
+    n = n_per + rank * 17  # ragged shards
+    keys = _make_keys(kind, dist_kind, n, rng)
+    pay = np.arange(n, dtype=np.int64) + rank * 10**9
+    kbits = 8 * key_size(kind)
+    bits = min(12, kbits)
+    ch = _chunk_hists(kind, keys, chunks, bits)
+    allh = [torch.zeros(ch.shape, dtype=torch.int64) for _ in range(world)]
+    dist.all_gather(allh, torch.from_numpy(ch.view(np.int64)))
+    allh = np.stack([h.numpy().view(np.uint64) for h in allh])
+    plan = shard.debug_plan(world, rank, chunks, rounds, kbits, allh, n)
+    gob = np.array(plan["group_of_bin"], np.int64)
+    # the partition (the device's srs_partition_device): per chunk, stable by group
+    top = _top(kind, keys, bits)
+    kcol = keys.view(KIND_UINT[kind]).astype(np.int64)  # bits, widened for gloo
+    part_k, part_p = np.empty_like(kcol), np.empty_like(pay)
+    cbnd = plan["chunk_bounds"]
+    for c in range(chunks):
+        a, b = cbnd[c], cbnd[c + 1]
+        order = a + np.argsort(gob[top[a:b]], kind="stable")
+        part_k[a:b], part_p[a:b] = kcol[order], pay[order]
+    total = plan["total"]
+    if plan["alias"]:
+        recv_k, recv_p = part_k, part_p
+    else:
+        recv_k, recv_p = np.zeros(total, np.int64), np.zeros(total, np.int64)
+    cols = [(part_k, recv_k), (part_p, recv_p)]
+    for post in plan["posts"]:
+        ops, landings = [], []
+        for op, peer, src, dst, cnt in post["msgs"]:
+            assert cnt > 0 and peer != rank or op == 2
+            for sbuf, rbuf in cols:
+                if op == 0:
+                    ops.append(dist.P2POp(dist.isend, torch.from_numpy(sbuf[src:src + cnt].copy()),
+                                          peer))
+                elif op == 1:
+                    t = torch.zeros(cnt, dtype=torch.int64)
+                    ops.append(dist.P2POp(dist.irecv, t, peer))
+                    landings.append((rbuf, dst, t))
+        if ops:
+            for req in dist.batch_isend_irecv(ops):
+                req.wait()
+        for rbuf, dst, t in landings:
+            rbuf[dst:dst + len(t)] = t.numpy()
+        for op, peer, src, dst, cnt in post["msgs"]:
+            if op == 2:
+                for sbuf, rbuf in cols:
+                    rbuf[dst:dst + cnt] = sbuf[src:src + cnt]
+    # the rounds: each a contiguous key range, sorted as the plan's segments
+    assert plan["rounds"][0]["start"] == 0 and plan["rounds"][-1]["end"] == total
+    ut = KIND_UINT[kind]
+    rk = recv_k.astype(ut)
+    for rd in plan["rounds"]:
+        a = rd["start"]
+        bnd = rd["bounds"]
+        kn = rd["known_bits"]
+        for s0, s1 in zip(bnd[:-1], bnd[1:]):
+            seg = rk[a + s0:a + s1].view(keys.dtype)
+            if kn and len(seg):
+                t = transformed_keys(kind, True, seg) >> np.uint64(kbits - kn)
+                assert (t == t[0]).all(), ("known bits not shared", rd)
+            order = a + s0 + np.argsort(transformed_keys(kind, True, seg), kind="stable")
+            rk[a + s0:a + s1] = rk[order]
+            recv_p[a + s0:a + s1] = recv_p[order]
+    return keys, pay, rk.view(keys.dtype), recv_p
+
+
+def _worker(rank, world, port, kind, dist_kind, n_per, chunks, rounds, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "simd-radix-sort_amd",
-                                    "python"))
-    from srs_amd.dist import ShardSorter
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        _run(rank, world, kind, n_per, dist_kind, q, bits, chunks)
+        keys, pay, ok, op = _run_rank(rank, world, kind, dist_kind, n_per, chunks, rounds)
+        outs = [None] * world
+        dist.all_gather_object(outs, (keys, pay, ok, op))
+        if rank == 0:
+            ink = np.concatenate([o[0] for o in outs])
+            inp = np.concatenate([o[1] for o in outs])
+            outk = np.concatenate([o[2] for o in outs])
+            outp = np.concatenate([o[3] for o in outs])
+            ref = np.argsort(transformed_keys(kind, True, ink), kind="stable")
+            q.put(("ok", bool(np.array_equal(outk.view(np.uint8), ink[ref].view(np.uint8))),
+                   bool(np.array_equal(outp, inp[ref]))))
     except Exception as e:  # report instead of hanging the parent
         q.put(("error", repr(e)))
         raise
@@ -84,186 +153,100 @@ def _worker(rank, world, port, kind, n_per, dist_kind, q, bits=8, chunks=4):
         dist.destroy_process_group()
 
 
-def _run(rank, world, kind, n_per, dist_kind, q, bits=8, chunks=4):
-    from srs_amd.dist import ShardSorter
-    if True:
-        rng = np.random.default_rng(100 + rank)
-        ut = KIND_UINT[kind]
-        n = n_per + rank * 17  # ragged shard sizes
-        if dist_kind == "uniform":
-            k = rng.integers(0, 2**63, n, dtype=np.uint64).astype(ut)
-        elif dist_kind == "skewed":  # everything in a few top buckets
-            k = (rng.integers(0, 3, n, dtype=np.uint64) << np.uint64(8 * key_size(kind) - 3)
-                 | rng.integers(0, 1000, n, dtype=np.uint64)).astype(ut)
-        else:  # all equal
-            k = np.full(n, 7, dtype=ut)
-        keys = torch.from_numpy(k.copy())
-        pay = torch.from_numpy(np.arange(n, dtype=np.int64) + rank * 10**9)
-        sorter = ShardSorter(NumpyShardOps(kind), n, [torch.int64], keys.dtype, "cpu", bits=bits,
-                             chunk_bytes=1024, chunks=chunks)  # many exchange rounds
-        # never more groups than histogram bins of the (clamped) key width
-        assert sorter.groups <= 1 << sorter.bits
-        ok, (op,) = sorter.sort(keys, [pay])
-        _check_phases(sorter, world, rank, n)
-        mine = ok.numpy().copy()
-        u = transformed_keys(kind, True, mine)
-        sorted_ok = bool(np.all(u[1:] >= u[:-1]))
-        # boundary check with the next rank, and a multiset check on rank 0
-        lohi = torch.tensor([int(u[0]) if len(u) else -1, int(u[-1]) if len(u) else -1],
-                            dtype=torch.float64)
-        allb = [torch.zeros(2, dtype=torch.float64) for _ in range(world)]
-        dist.all_gather(allb, lohi)
-        gathered_k = [None] * world
-        gathered_p = [None] * world
-        dist.all_gather_object(gathered_k, mine.tolist())
-        dist.all_gather_object(gathered_p, op.numpy().tolist())
-        inputs = [None] * world
-        dist.all_gather_object(inputs, (k.tolist(), pay.numpy().tolist()))
-        if rank == 0:
-            outk = np.concatenate([np.array(g, dtype=ut) for g in gathered_k])
-            outp = np.concatenate([np.array(g, dtype=np.int64) for g in gathered_p])
-            ink = np.concatenate([np.array(i[0], dtype=ut) for i in inputs])
-            inp = np.concatenate([np.array(i[1], dtype=np.int64) for i in inputs])
-            ref = np.argsort(transformed_keys(kind, True, ink), kind="stable")
-            q.put((sorted_ok, np.array_equal(outk, ink[ref]),
-                   sorted(zip(outk.tolist(), outp.tolist())) ==
-                   sorted(zip(ink.tolist(), inp.tolist())),
-                   [b.tolist() for b in allb]))
-        else:
-            q.put((sorted_ok, True, True, None))
-
-
-def _check_phases(sorter, world, rank, n):
-    """bench.py's N > 1 line carries ShardSorter.phases() of every rank: the
-    stamps of each phase, the bytes sent to each peer per round, the implied
-    link rate and the DESIGN.md §7 model's prediction (JSON-serializable)."""
-    import json
-    ph = sorter.phases()
-    json.dumps(ph)
-    st = ph["stamps_ms"]
-    R = sorter.rounds
-    C = sorter.chunks
-    need = ["start", "hist", "plan", "end"] + [f"partition{c}" for c in range(C)] + \
-        [f"round{r}_recv" for r in range(R)]
-    assert all(k in st for k in need), (need, st)
-    assert st["start"] == 0 and all(v >= 0 for v in st.values())
-    assert st["plan"] >= st["hist"] and st["end"] >= st[f"round{R - 1}_recv"]
-    b = ph["bytes_to_peer_per_round"]
-    assert len(b) == R and all(len(x) == world and x[rank] == 0 for x in b)
-    tot = sum(sum(x) for x in b)
-    assert tot <= n * sorter.rec_bytes
-    assert ph["busiest_link_bytes"] == max(sum(x[d] for x in b) for d in range(world))
-    assert set(ph["model"]) == {"T_ms_at_50GBs", "T_ms_at_77GBs"}
-    assert ph["measured_T_ms"] == st["end"]
-
-
-def _run_world(world, kind, dist_kind, bits=8, chunks=4):
+def _run_world(world, kind, dist_kind, chunks=4, rounds=3, n_per=3000):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, kind, 3000, dist_kind, q, bits,
-                                               chunks))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, kind, dist_kind, n_per, chunks,
+                                               rounds, q))
              for r in range(world)]
     for p in procs:
         p.start()
-    res = [q.get(timeout=120) for _ in procs]
+    res = q.get(timeout=180)
     for p in procs:
         p.join(timeout=60)
+    assert res[0] == "ok", res
+    assert res[1] and res[2], res
+    for p in procs:
         assert p.exitcode == 0
-    assert not [r for r in res if r[0] == "error"], res
-    for sorted_ok, keys_ok, multiset_ok, bounds in res:
-        assert sorted_ok and keys_ok and multiset_ok
-    b = [r[3] for r in res if r[3] is not None][0]
-    nonempty = [x for x in b if x[0] >= 0]
-    for a, c in zip(nonempty, nonempty[1:]):
-        assert a[1] <= c[0]  # last key of rank r <= first key of rank r+1
 
 
 @pytest.mark.parametrize("world", [2, 3, 4])
 @pytest.mark.parametrize("dist_kind", ["uniform", "skewed", "equal"])
-def test_shard_sort_gloo(world, dist_kind):
+def test_shard_plan_gloo(world, dist_kind):
     _run_world(world, 6, dist_kind)
 
 
-@pytest.mark.parametrize("chunks", [1, 3])
-def test_shard_sort_gloo_partition_chunks(chunks):
-    """the partition in 1 or 3 input chunks (the first round's messages of a
-    chunk overlap the next chunk's partition): same result, stable"""
-    _run_world(3, 6, "skewed", chunks=chunks)
+@pytest.mark.parametrize("chunks,rounds", [(1, 1), (3, 8), (8, 16)])
+def test_shard_plan_gloo_chunks_rounds(chunks, rounds):
+    """partition chunks (each chunk's round-0 messages posted after its
+    partition) and exchange rounds: same result, stable"""
+    _run_world(3, 6, "skewed", chunks=chunks, rounds=rounds)
 
 
-@pytest.mark.parametrize("kind", [0, 3])  # u8, i16: keys narrower than the default 12 bits
+@pytest.mark.parametrize("kind", [0, 3, 8])  # u8, i16 (narrower than 12 bits), f32
 @pytest.mark.parametrize("dist_kind", ["uniform", "skewed"])
-def test_shard_sort_gloo_narrow_keys(kind, dist_kind):
-    _run_world(2, kind, dist_kind, bits=12)
+def test_shard_plan_gloo_key_kinds(kind, dist_kind):
+    _run_world(2, kind, dist_kind)
 
 
-def test_balanced_split_is_monotone_and_balanced():
-    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "simd-radix-sort_amd",
-                                    "python"))
-    from srs_amd.dist import balanced_split
-    h = torch.tensor([5, 0, 100, 3, 3, 3, 50, 0, 0, 36], dtype=torch.int64)
-    for w in (1, 2, 3, 8):
-        p = balanced_split(h, w)
-        assert p.dtype == torch.int32 and len(p) == len(h)
-        assert bool((p[1:] >= p[:-1]).all()) and int(p.min()) >= 0 and int(p.max()) < w
-    u = balanced_split(torch.full((256,), 10, dtype=torch.int64), 8)
-    assert torch.bincount(u.long(), minlength=8).tolist() == [32] * 8
+@pytest.mark.parametrize("chunks,rounds", [(1, 4), (4, 4)])
+def test_shard_plan_one_rank(chunks, rounds):
+    """world 1: one chunk = the partitioned buffer is the receive buffer
+    (alias, each group its own segment); several chunks = own-piece copies"""
+    _run_world(1, 6, "uniform", chunks=chunks, rounds=rounds)
 
 
-class _BadCountOps(NumpyShardOps):
-    """Reports wrong group sizes for the second partition chunk (after the
-    first chunk's messages are posted)."""
-
-    def __init__(self, kind):
-        super().__init__(kind)
-        self.calls = 0
-
-    def partition(self, *a, **k):
-        got = super().partition(*a, **k)
-        self.calls += 1
-        if self.calls == 2:
-            got = list(got)
-            got[0] += 1
-        return got
-
-
-def _bad_worker(rank, world, port, q):
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "simd-radix-sort_amd",
-                                    "python"))
-    from srs_amd.dist import ShardSorter
-    dist.init_process_group("gloo", rank=rank, world_size=world)
-    rng = np.random.default_rng(rank)
-    n = 4000
-    keys = torch.from_numpy(rng.integers(0, 2**63, n, dtype=np.uint64))
-    pay = torch.arange(n, dtype=torch.int64)
-    ops = _BadCountOps(6) if rank == 0 else NumpyShardOps(6)
-    sorter = ShardSorter(ops, n, [torch.int64], keys.dtype, "cpu", bits=8, chunk_bytes=1024,
-                         chunks=3)
-    try:
-        sorter.sort(keys, [pay])
-        q.put((rank, "finished"))
-    except Exception as e:
-        q.put((rank, type(e).__name__ + ": " + str(e)[:200]))
-    dist.destroy_process_group()
-
-
-def test_shard_sort_failure_does_not_hang_peers():
-    """a rank that finds its partition sizes wrong after posting
-    messages keeps to the agreed message plan, so its peers are not left
-    waiting on receives, and every rank raises at the end."""
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_bad_worker, args=(r, 2, port, q)) for r in range(2)]
-    for p in procs:
-        p.start()
-    res = dict(q.get(timeout=120) for _ in procs)
-    for p in procs:
-        p.join(timeout=60)
-    assert "partition sizes differ" in res[0], res
-    assert "partition sizes differ" in res[1] and "another rank" in res[1], res
-    for p in procs:
-        assert p.exitcode == 0
+# ---- the plan itself, every rank in one process ------------------------------
+@pytest.mark.parametrize("world,chunks,rounds,kind", [
+    (2, 8, 8, 6), (3, 4, 16, 6), (8, 8, 8, 6), (8, 16, 64, 6), (5, 2, 3, 0), (4, 8, 8, 2)])
+def test_shard_plan_messages_pair_up(world, chunks, rounds, kind):
+    """For every pair of ranks the sends of one match the receives of the
+    other in posting order and size; every rank's receives and own copies
+    tile its receive buffer exactly once; every partitioned record is sent
+    or copied exactly once; rounds are contiguous and in key order."""
+    shard = _shard()
+    rng = np.random.default_rng(world * 100 + chunks)
+    kbits = 8 * key_size(kind)
+    bits = min(12, kbits)
+    nb = 1 << bits
+    ns = [int(x) for x in rng.integers(0, 5000, world)]
+    hs = np.zeros((world, chunks, nb), np.uint64)
+    for s in range(world):
+        top = np.minimum(rng.geometric(0.002, ns[s]) - 1, nb - 1)  # skewed bins
+        for c in range(chunks):
+            a, b = ns[s] * c // chunks, ns[s] * (c + 1) // chunks
+            hs[s, c] = np.bincount(top[a:b], minlength=nb)
+    plans = [shard.debug_plan(world, r, chunks, rounds, kbits, hs, ns[r]) for r in range(world)]
+    assert all(p["group_of_bin"] == plans[0]["group_of_bin"] for p in plans)
+    assert all(p["rank_of_group"] == plans[0]["rank_of_group"] for p in plans)
+    assert sum(p["total"] for p in plans) == sum(ns)
+    rog = plans[0]["rank_of_group"]
+    assert rog == sorted(rog)
+    nposts = len(plans[0]["posts"])
+    assert all(len(p["posts"]) == nposts for p in plans)
+    for i in range(nposts):
+        for s in range(world):
+            for d in range(world):
+                if s == d:
+                    continue
+                sends = [m[4] for m in plans[s]["posts"][i]["msgs"] if m[0] == 0 and m[1] == d]
+                recvs = [m[4] for m in plans[d]["posts"][i]["msgs"] if m[0] == 1 and m[1] == s]
+                assert sends == recvs, (i, s, d)
+    for r, p in enumerate(plans):
+        cover = np.zeros(p["total"], np.int64)
+        used = np.zeros(ns[r], np.int64)
+        for post in p["posts"]:
+            for op, peer, src, dst, cnt in post["msgs"]:
+                if op in (1, 2):
+                    cover[dst:dst + cnt] += 1
+                if op in (0, 2):
+                    used[src:src + cnt] += 1
+        if not p["alias"]:
+            assert (cover == 1).all() and (used == 1).all(), r
+        rd = p["rounds"]
+        assert [x["start"] for x in rd[1:]] == [x["end"] for x in rd[:-1]]
+        for x in rd:
+            assert x["bounds"][0] == 0 and x["bounds"][-1] == x["end"] - x["start"] or \
+                x["end"] == x["start"]
+            assert 0 <= x["known_bits"] < kbits
