@@ -1069,7 +1069,10 @@ int plan_balanced_level(Workspace* W, const Request& R, const SortDesc& d, bool*
     top9max = std::max(top9max, t);
   }
   if (total == 0) return SRS_OK;
-  if (!R.aos) {
+  // (not with canon_zero: the range level's exact min / max are taken over
+  // the raw transformed keys, while its passes map -0.0 onto +0.0's code,
+  // which can lie outside them)
+  if (!R.aos && !d.canon_zero) {
     std::vector<KeyCluster> cl;
     bool ok = true;
     for (int b = 0; b < 65536 && ok; b++) {  // (stops at the first cluster too many or too wide)

@@ -120,3 +120,59 @@ def test_gaussian_aos16_vs_reference(torch):
     ref_sort_aos(srs_amd.KEY_I64, True, rec)
     torch.cuda.synchronize()
     assert np.array_equal(out.cpu().numpy(), rec)
+
+
+# ---- several key clusters, outliers, stability -----------------
+def _clustered(seed, n, centers, width, outliers=()):
+    """u64 keys in narrow clusters around `centers` (+- width), plus a few
+    outlier keys placed where a sample of the input is unlikely to see them
+    (single keys at fixed positions): they widen the exact min / max the range
+    level computes beyond the sampled clusters."""
+    rng = np.random.default_rng(seed)
+    which = rng.integers(0, len(centers), n)
+    c = np.array(centers, dtype=np.uint64)[which]
+    k = c - np.uint64(width) + rng.integers(0, 2 * width, n, dtype=np.uint64)
+    for i, v in enumerate(outliers):
+        k[(i * 7919 + 13) % n] = np.uint64(v)
+    return k
+
+
+@pytest.mark.parametrize("case", ["3_clusters", "4_clusters_both_ends", "outliers",
+                                  "empty_middle"])
+def test_range_level_clusters_vs_reference(torch, case):
+    """The range level with 2-4 key clusters, unsigned keys at both ends of
+    the range, empty ranges between clusters, and unsampled outliers that
+    widen the exact min / max: bit-equal to the reference at 2^25 + 1234."""
+    top = (1 << 64) - 1
+    if case == "3_clusters":
+        k = _clustered(21, N, [1 << 40, 1 << 50, 1 << 60], 3000)
+    elif case == "4_clusters_both_ends":
+        k = _clustered(22, N, [4000, 1 << 62, 3 << 62, top - 4000], 3000)
+    elif case == "outliers":
+        k = _clustered(23, N, [1 << 41, 5 << 59], 2000,
+                       outliers=[0, 1, top, top - 1, 1 << 63, (1 << 52) + 17])
+    else:  # two clusters with nothing between them but one outlier
+        k = _clustered(24, N, [1000, top - 1000], 900, outliers=[1 << 63])
+    _sort_soa_both(torch, srs_amd.KEY_U64, k)
+
+
+@pytest.mark.parametrize("case", ["gaussian", "3_clusters", "outliers"])
+def test_range_level_is_stable(torch, case):
+    """Index payloads and many duplicate keys: the GPU output equals a stable
+    CPU argsort (the home-write path of the range level keeps input order)."""
+    from srs_testlib import transformed_keys
+    if case == "gaussian":
+        k = _keys("gaussian", np.int64, seed=31)
+        kind = srs_amd.KEY_I64
+    else:
+        k = _clustered(32, N, [1 << 40, 1 << 50, 1 << 60], 300,
+                       outliers=[0, (1 << 64) - 1] if case == "outliers" else ())
+        kind = srs_amd.KEY_U64
+    idx = np.arange(N, dtype=np.int64)
+    kd = torch.from_numpy(k.view(np.int64).copy()).cuda()
+    pd = torch.from_numpy(idx.copy()).cuda()
+    srs_amd.sort_device(kd, pd, key_kind=kind)
+    order = np.argsort(transformed_keys(kind, True, k), kind="stable")
+    torch.cuda.synchronize()
+    assert np.array_equal(kd.cpu().numpy().view(k.dtype), k[order])
+    assert np.array_equal(pd.cpu().numpy(), idx[order])
