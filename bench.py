@@ -66,6 +66,9 @@ def parse():
                     help="shard exchange rounds (srs_shard_set_options; 0 = library default)")
     ap.add_argument("--chunks", type=int, default=0,
                     help="shard partition chunks (srs_shard_set_options; 0 = library default)")
+    ap.add_argument("--t1-ms", type=float, default=21.245,
+                    help="one-GPU step time the --shard world-1 line's 8-GPU model compares "
+                         "against (default: BENCH_r04's C1)")
     ap.add_argument("--alloc-steps", type=int, default=3,
                     help="world 1: extra steps with outputs from torch's allocator and in place "
                          "on a torch array (ms_per_step_plain_alloc / _inplace; 0 = skip)")
@@ -516,6 +519,13 @@ def measure(cfg_name, args, torch, srs_amd, dist, dev, rank, world, shard):
         # model's prediction for those bytes
         mine = sorter.phases()
         mine["rank"] = rank
+        if world == 1:
+            # the head and tail measured here, in DESIGN.md §7's 8-GPU model
+            # (T(1) = the plain one-GPU step of the same shape, 21.2 ms for C1
+            # in BENCH_r04; pass --t1-ms to use another)
+            mine["t8_model"] = shard_mod.t8_model(
+                mine.get("head_ms") or 0.0, mine.get("tail_ms") or 0.0, args.t1_ms, n=n,
+                rec_bytes=rec_bytes)
         allph = [None] * world
         dist.all_gather_object(allph, mine)
         phases = allph

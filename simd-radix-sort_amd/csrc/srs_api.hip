@@ -1138,12 +1138,25 @@ int plan_balanced_level(Workspace* W, const Request& R, const SortDesc& d, bool*
   return SRS_OK;
 }
 
+// The tile-pair scatter (scatter_pair_kernel) takes the
+// shapes whose runs per tile are shortest: 4-byte keys with C2's pair word
+// (SRS_PAIR_TILES=0 turns it off, =1 also takes the key + one column shapes
+// of 4- and 8-byte keys, A/B runs).
+bool pair_tiles_ok(const SortDesc& d, int ks) {
+  const char* e = getenv("SRS_PAIR_TILES");
+  const int mode = e && *e ? atoi(e) : 2;
+  if (mode == 0 || d.canon_zero || (ks != 4 && ks != 8)) return false;
+  if (d.pair) return ks == 4 && d.ncols == 3;
+  return mode == 1 && d.ncols <= 2;
+}
+
 struct LevelState {
   int64_t nbig, n_local, n_local2, n_copy;
   int cur;
   int ncols;               // columns moved with the keys (SortDesc::ncols)
   int tmp2;                // SortDesc::tmp2
   int64_t known_len = -1;  // the length of the single big segment, when the host knows it
+  int pair_tiles = 0;      // the scatter takes two count tiles per workgroup (pair_tiles_ok)
   int level = 0;           // global levels run so far (per-level timing names)
 };
 
@@ -1263,9 +1276,13 @@ int run_level(Workspace* W, int ks, const SortDesc* d_desc, LevelState& S, int f
     HIP_TRY(hipMemsetAsync(g_lb_status, 0, (size_t)ntiles * kMaxBins * 4, st));
   {
     TimedScope ts("scatter", (double)0, st, lv);
-    launch_scatter(ks, d_desc, plan, tile_seg, (uint64_t*)W->offs.p,
-                   offs32 ? (const uint32_t*)W->offs.p : nullptr, ntiles, lut, S.ncols, st,
-                   M.gt);
+    if (S.pair_tiles && lut != 1)
+      launch_scatter_pairs(ks, d_desc, plan, tile_seg, (uint64_t*)W->offs.p,
+                           offs32 ? (const uint32_t*)W->offs.p : nullptr, ntiles, lut, st, M.gt);
+    else
+      launch_scatter(ks, d_desc, plan, tile_seg, (uint64_t*)W->offs.p,
+                     offs32 ? (const uint32_t*)W->offs.p : nullptr, ntiles, lut, S.ncols, st,
+                     M.gt);
   }
   if (M.mode == 1) {
     // the buckets become the next level's segments (logical starts: where
@@ -1674,6 +1691,7 @@ int run_sort(Workspace* W, const Request& R, hipStream_t st) {
     W->h_ctr->local_elems = to_local ? (uint64_t)n : 0;
   }
   LevelState S{n_big, n_local, n_local2, n_copy, 0, d.ncols, d.tmp2};
+  S.pair_tiles = pair_tiles_ok(d, ks) ? 1 : 0;
   if (R.nsegs == 0 && n_big == 1) S.known_len = n;
   int level = 0;
   // Stripe first level: large plain SoA sorts partition

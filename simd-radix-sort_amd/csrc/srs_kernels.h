@@ -40,6 +40,11 @@ void launch_scatter(int key_size, const SortDesc* d, const SegPlan* plan,
                     const int32_t* tile_seg, const uint64_t* offs, const uint32_t* offs32,
                     int64_t ntiles, int lut, int ncols, hipStream_t st,
                     const GTile* gt = nullptr);
+// the same level's scatter with two count tiles per workgroup (lut 0 or 2;
+// 4- or 8-byte keys; the key plus one column or C2's pair word; no canon zero)
+void launch_scatter_pairs(int key_size, const SortDesc* d, const SegPlan* plan,
+                          const int32_t* tile_seg, const uint64_t* offs, const uint32_t* offs32,
+                          int64_t ntiles, int lut, hipStream_t st, const GTile* gt = nullptr);
 // stripe first level -> the second level's segment list (W->big, n_big),
 // tile counts (nt_over) and gathered tile table (gt); see GTile
 void launch_stripe_tables(const uint32_t* prun, int64_t nstripes, int nb, uint32_t* ptile,

@@ -1704,6 +1704,213 @@ __global__ __launch_bounds__(kScatterThreads, SRS_SCATTER_WAVES_PER_EU) void sca
 }
 
 // ---------------------------------------------------------------------------
+// scatter of two count tiles per workgroup ("tile pairs", 8192 records)
+// ---------------------------------------------------------------------------
+// The scatter's cost follows the number of partially written 64-byte blocks
+// (the runs per digit and tile, not the bytes). Two
+// consecutive count tiles of one segment ranked together write each
+// bucket's run per workgroup twice as long: C2's 4-byte keys 64-byte runs
+// instead of 32, its payload words 128 instead of 64. The count pass and
+// the scans are unchanged: tile b's offsets are tile a's plus a's counts, so
+// ranking a's records before b's (waves 0-3 hold tile a, waves 4-7 tile b)
+// and adding tile a's offsets gives the same stable result. 512 threads x 16
+// records; the LDS holds one 8-byte slot per record (the 4-byte keys use
+// half of it), 8 per-wave counter rows and the bucket bases: 79 KB with the
+// small digit table, two workgroups per CU. Digits are recomputed from the
+// staged key instead of staged. Columns: the key plus one column, or the
+// key plus C2's pair word (SortDesc::pair).
+constexpr int kPairThreads = 512;
+constexpr int kPairItems = 16;
+constexpr int kPairTile = 2 * kTile;
+static_assert(kPairThreads * kPairItems == kPairTile, "tile pair shape");
+static_assert(kPairThreads >= kMaxBins, "the pair scan gives one bin per thread");
+
+struct PairLds {
+  uint64_t sval[kPairTile];
+  alignas(8) uint16_t wc[kPairThreads / 64][kMaxBins];
+  uint16_t bin_start[kMaxBins];  // tile-pair offsets <= 8192 fit 16 bits
+  int64_t gdst[kMaxBins];
+  uint32_t scan_sh[kPairThreads / 64 + 1];
+};
+
+// a strip of IT slots into registers of type T (load_strip's layout)
+template <int IT, typename T>
+__device__ __forceinline__ void load_strip_t(T (&dst)[IT], const char* src, uint32_t w,
+                                             uint32_t st, int64_t first, int ebase, int cnt) {
+  uint64_t tmp[IT];
+  load_strip<IT>(tmp, src, w, st, first, ebase, cnt);
+#pragma unroll
+  for (int k = 0; k < IT; k++) dst[k] = (T)tmp[k];
+}
+
+template <typename KT, typename U, int LUT>
+__device__ __forceinline__ void scatter_pair_tiles(
+    const SortDesc* __restrict__ desc, const SegPlan* __restrict__ plan, PairLds& L,
+    const int32_t* __restrict__ tile_seg, const uint64_t* __restrict__ offs,
+    const uint32_t* __restrict__ offs32, const GTile* __restrict__ gt, int64_t ta, int64_t tb,
+    const DigitLut& lut) {
+  constexpr int NT = kPairThreads;
+  constexpr int IT = kPairItems;
+  constexpr int NW = NT / 64;
+  constexpr int KW = sizeof(KT) >= 8 ? 8 : 4;  // (key register width)
+  typedef typename std::conditional<KW == 8, uint64_t, uint32_t>::type KR;
+  const SegPlan P = plan[tile_seg[ta]];
+  int64_t base[2] = {0, 0};
+  int cnt[2] = {0, 0};
+  for (int h = 0; h < 2; h++) {
+    const int64_t t = h ? tb : ta;
+    if (t < 0) continue;
+    if (gt) {
+      base[h] = gt[t].src;
+      cnt[h] = gt[t].cnt;
+    } else {
+      const int64_t tl = t - P.tile_base;
+      base[h] = P.start + tl * kTile;
+      const int64_t rem = P.len - tl * kTile;
+      cnt[h] = P.skip ? 0 : (int)std::min<int64_t>(rem, kTile);
+    }
+  }
+  const int total = cnt[0] + cnt[1];
+  if (total == 0) return;
+  const uint32_t wave = threadIdx.x >> 6;
+  const int half = (int)(wave >> 2);
+  const int64_t mybase = half ? base[1] : base[0];
+  const int mycnt = half ? cnt[1] : cnt[0];
+  const int ebase = (int)(wave & 3) * IT * 64 + (int)lane_id();
+  const int ncols = desc->ncols;
+  const bool pair = desc->pair != 0;
+  const bool pair_src = pair && (P.buf == BUF_TMP || P.buf == BUF_TMP2);
+
+  // loads: the key column, then the payload column (or the pair word)
+  KR v0[IT];
+  uint64_t v1[IT];
+  load_strip_t<IT>(v0, desc->cols[0].base[P.buf], desc->cols[0].width,
+                   desc->cols[0].stride[P.buf], mybase, ebase, mycnt);
+  if (ncols > 1)
+    load_strip<IT>(v1, desc->cols[1].base[P.buf], pair_src ? 8u : desc->cols[1].width,
+                   desc->cols[1].stride[P.buf], mybase, ebase, mycnt);
+  if (pair && !pair_src) {  // two 4-byte columns from the caller's arrays: joined here
+    uint32_t v2[IT];
+    load_strip_t<IT>(v2, desc->cols[2].base[P.buf], 4u, desc->cols[2].stride[P.buf], mybase,
+                     ebase, mycnt);
+#pragma unroll
+    for (int k = 0; k < IT; k++) v1[k] = (v1[k] & 0xFFFFFFFFull) | ((uint64_t)v2[k] << 32);
+  }
+  int64_t my_off = 0;
+  const uint32_t nb = 1u << P.bits;
+  if (threadIdx.x < nb)
+    my_off = offs32 ? (int64_t)offs32[ta * kMaxBins + threadIdx.x]
+                    : (int64_t)offs[ta * kMaxBins + threadIdx.x];
+
+  const uint32_t mask = nb - 1;
+  Xform<U, false> xf;
+  xf.init(*desc);
+  const int kbytes = desc->key_bits >> 3;
+  const U kmask = kbytes >= (int)sizeof(U) ? (U)~(U)0 : (U)(((uint64_t)1 << (8 * kbytes)) - 1);
+#pragma unroll
+  for (int i = 0; i < kMaxBins / 256; i++)
+    ((uint64_t*)&L.wc[wave][0])[i * 64 + lane_id()] = 0;
+  auto valid = [&](int k) -> bool { return ebase + k * 64 < mycnt; };
+  uint32_t dg[IT];
+#pragma unroll
+  for (int k = 0; k < IT; k++) dg[k] = pass_digit<LUT>(xf((U)v0[k] & kmask), P.shift, mask, lut);
+  uint32_t pos[IT];
+  wlms_rank_fn<IT, kMaxDigitBits, true>([&](int k) { return dg[k]; }, valid, P.bits,
+                                        &L.wc[wave][0], pos);
+  lds_barrier();
+  {  // per-bin totals over the waves (tile a's waves first) -> wave offsets; scan
+    const uint32_t my_bin = threadIdx.x;
+    uint32_t tsum = 0;
+    if (my_bin < nb) {
+#pragma unroll
+      for (int w = 0; w < NW; w++) {
+        const uint32_t c = L.wc[w][my_bin];
+        L.wc[w][my_bin] = (uint16_t)tsum;
+        tsum += c;
+      }
+    }
+    const uint32_t ex = block_excl_scan_1b<NT>(tsum, L.scan_sh);
+    if (my_bin < nb) {
+      L.bin_start[my_bin] = (uint16_t)ex;
+      L.gdst[my_bin] = P.start + my_off - (int64_t)ex;
+    }
+  }
+  lds_barrier();
+  KR* skey = (KR*)L.sval;
+#pragma unroll
+  for (int k = 0; k < IT; k++)
+    if (valid(k)) {
+      const uint32_t d = dg[k];
+      pos[k] = L.bin_start[d] + L.wc[wave][d] + pos[k];
+      skey[pos[k]] = v0[k];
+    }
+  lds_barrier();
+  // the key column: slot j's bucket from its staged key
+  uint16_t dout[IT];
+  {
+    char* out = desc->cols[0].base[P.dst];
+    const uint32_t st = desc->cols[0].stride[P.dst];
+    with_width(desc->cols[0].width, [&](auto W_) {
+#pragma unroll
+      for (int i = 0; i < IT; i++) {
+        const int j = i * NT + (int)threadIdx.x;
+        dout[i] = 0;
+        if (j < total) {
+          const KR x = skey[j];
+          const uint32_t d = pass_digit<LUT>(xf((U)x & kmask), P.shift, mask, lut);
+          dout[i] = (uint16_t)d;
+          stw<decltype(W_)::value>(out + ((int64_t)j + L.gdst[d]) * (int64_t)st, (uint64_t)x);
+        }
+      }
+    });
+  }
+  if (ncols < 2) return;
+  lds_barrier();  // every key slot has been read
+#pragma unroll
+  for (int k = 0; k < IT; k++)
+    if (valid(k)) L.sval[pos[k]] = v1[k];
+  lds_barrier();
+  {
+    char* out = desc->cols[1].base[P.dst];
+    const bool pair_dst = pair && (P.dst == BUF_TMP || P.dst == BUF_TMP2);
+    const uint32_t w1 = pair_dst ? 8u : desc->cols[1].width;
+    const uint32_t st = pair_dst ? 8u : desc->cols[1].stride[P.dst];
+    with_width(w1, [&](auto W_) {
+#pragma unroll
+      for (int i = 0; i < IT; i++) {
+        const int j = i * NT + (int)threadIdx.x;
+        if (j < total)
+          stw<decltype(W_)::value>(out + ((int64_t)j + L.gdst[dout[i]]) * (int64_t)st, L.sval[j]);
+      }
+    });
+  }
+}
+
+// One pair of count tiles (2w, 2w + 1) per workgroup, XCD-aware order; a
+// pair that straddles two segments is scattered as two single tiles.
+template <typename KT, typename U, int LUT>
+__global__ __launch_bounds__(kPairThreads, 4) void scatter_pair_kernel(
+    const SortDesc* __restrict__ desc, const SegPlan* __restrict__ plan,
+    const int32_t* __restrict__ tile_seg, const uint64_t* __restrict__ offs,
+    const uint32_t* __restrict__ offs32, const GTile* __restrict__ gt, int64_t ntiles) {
+  __shared__ PairLds L;
+  __shared__ alignas(16) uint16_t slut[kLutLdsEntries<LUT>];
+  const int64_t ta = 2 * xcd_remap(blockIdx.x, gridDim.x);
+  const int64_t tb = ta + 1;
+  const DigitLut lut = stage_lut<LUT, kPairThreads>(desc, slut);
+  if (LUT) lds_barrier();  // publishes the staged digit table
+  if (tb < ntiles && tile_seg[tb] == tile_seg[ta]) {
+    scatter_pair_tiles<KT, U, LUT>(desc, plan, L, tile_seg, offs, offs32, gt, ta, tb, lut);
+  } else {
+    scatter_pair_tiles<KT, U, LUT>(desc, plan, L, tile_seg, offs, offs32, gt, ta, -1, lut);
+    if (tb < ntiles) {
+      lds_barrier();  // (the first tile's slots have all been read)
+      scatter_pair_tiles<KT, U, LUT>(desc, plan, L, tile_seg, offs, offs32, gt, tb, -1, lut);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // local: one workgroup sorts one segment (<= CAP keys) in LDS
 // ---------------------------------------------------------------------------
 // Finishes the recursion for a segment that fits in LDS (the reference's
@@ -3426,6 +3633,23 @@ void launch_scatter(int key_size, const SortDesc* d, const SegPlan* plan,
   SRS_KEY_DISPATCH(key_size, CALL)
 #undef CALL
 #undef CALL_L
+}
+
+void launch_scatter_pairs(int key_size, const SortDesc* d, const SegPlan* plan,
+                          const int32_t* tile_seg, const uint64_t* offs, const uint32_t* offs32,
+                          int64_t ntiles, int lut, hipStream_t st, const GTile* gt) {
+  const unsigned grid = (unsigned)((ntiles + 1) / 2);
+#define CALL_P(KT, U, LK)                                                            \
+  scatter_pair_kernel<KT, U, LK><<<grid, kPairThreads, 0, st>>>(d, plan, tile_seg, offs, \
+                                                               offs32, gt, ntiles)
+  if (key_size == 4) {
+    if (lut == 2) CALL_P(uint32_t, uint32_t, 2);
+    else CALL_P(uint32_t, uint32_t, 0);
+  } else {
+    if (lut == 2) CALL_P(uint64_t, uint64_t, 2);
+    else CALL_P(uint64_t, uint64_t, 0);
+  }
+#undef CALL_P
 }
 
 void launch_stripe_tables(const uint32_t* prun, int64_t nstripes, int nb, uint32_t* ptile,

@@ -247,3 +247,22 @@ def link_figures(rep: dict, link_gbs_model=(50.0, 64.0, 77.0)) -> dict:
                         for g in link_gbs_model}
         out["measured_T_ms"] = st.get("end")
     return out
+
+
+def t8_model(head_ms: float, tail_ms: float, t1_ms: float, n: int = 10**9,
+             rec_bytes: int = 16, world: int = 8, link_gbs=(50.0, 64.0, 77.0)) -> dict:
+    """DESIGN.md §7's weak-scaling model from measured pieces: at `world`
+    ranks of n records each, every link carries n * rec_bytes / world bytes
+    each way; T(world) = head + those bytes / link rate + tail (the HBM work
+    of the rounds hides under the transfers). Also the per-link rate at which
+    `world` GPUs reach 6/8 of perfect scaling (6x at 8) against a one-GPU
+    step of t1_ms, given this head and tail."""
+    link_bytes = n * rec_bytes / world
+    out = {f"T{world}_ms_at_{int(g)}GBs": round(head_ms + link_bytes / (g * 1e9) * 1e3 + tail_ms, 3)
+           for g in link_gbs}
+    budget = t1_ms / 0.75  # world * n / T >= 0.75 * world * n / T1
+    room = budget - head_ms - tail_ms
+    out["budget_ms_for_6x"] = round(budget, 3)
+    out["link_gbs_needed_for_6x"] = round(link_bytes / (room * 1e-3) / 1e9, 1) if room > 0 else None
+    out["link_bytes_each_way"] = link_bytes
+    return out
