@@ -109,10 +109,12 @@ def test_hot_kernels_keep_their_occupancy():
     """The occupancy the tuning relies on: two 16-wave scatter
     workgroups per CU need <= 64 VGPRs (8 waves/SIMD), with or without the
     24 KB digit table; count 8 waves/SIMD (6 for digit-table passes);
-    the small local class 6 waves/SIMD (3 workgroups of 8 waves); nothing
-    on the hot path spills to scratch."""
+    the small local class 6 waves/SIMD (3 workgroups of 8 waves); the
+    tile-pair scatter two 8-wave workgroups per CU (4 waves/SIMD, <= 80 KB of
+    LDS each); nothing on the hot path spills to scratch."""
     res = _kernel_resources()
-    need = {"scatter_kernel": 8, "count_kernel": 8, "local_kernelI": None}
+    need = {"scatter_kernel": 8, "count_kernel": 8, "local_kernelI": None,
+            "scatter_pair_kernel": 4}
     seen = set()
     for name, r in res.items():
         for key, occ in need.items():
@@ -128,6 +130,8 @@ def test_hot_kernels_keep_their_occupancy():
             if key == "count_kernel" and "ImmLi2E" in name:
                 occ = 6  # the 8-byte range level: 7 or 8 waves spill VGPRs to scratch
             assert r["Occupancy"] >= occ, (name, r)
+            if key == "scatter_pair_kernel":
+                assert r["LDS"] * 2 <= 160 * 1024, (name, r)
     assert seen == set(need)
 
 

@@ -1,0 +1,10 @@
+set -o pipefail
+mkdir -p gpurun_out/r5b
+T="timeout -k 10"
+$T 900 python -u -m pytest tests/test_shard_gpu.py tests/test_cpp_dropin.py tests/test_gpu_keyrange.py tests/test_gpu_ref_full.py -x -v --timeout 300 --timeout-method thread -m gpu > gpurun_out/r5b/t.txt 2>&1 || exit 1
+for i in 1 2; do
+  SRS_PAIR_TILES=0 $T 200 python -u bench.py --config c2 --steps 10 --cpu-sample 0 --extra none --alloc-steps 0 > gpurun_out/r5b/c2_off_$i.json 2>gpurun_out/r5b/c2_off_$i.err || exit 2
+  $T 200 python -u bench.py --config c2 --steps 10 --cpu-sample 0 --extra none --alloc-steps 0 > gpurun_out/r5b/c2_on_$i.json 2>gpurun_out/r5b/c2_on_$i.err || exit 3
+done
+$T 300 python -u bench.py --shard --steps 5 --warmup 1 --cpu-sample 0 --extra none --alloc-steps 0 > gpurun_out/r5b/shard_w1_default.json 2> gpurun_out/r5b/shard_w1_default.err || exit 4
+$T 300 python -u bench.py --shard --steps 5 --warmup 1 --cpu-sample 0 --extra none --alloc-steps 0 --rounds 16 --chunks 8 > gpurun_out/r5b/shard_w1_r16c8.json 2> gpurun_out/r5b/shard_w1_r16c8.err || exit 5
