@@ -1,7 +1,8 @@
+# round 5, GPU call b: the whole GPU suite, C2 tile-pair A/B, shard world-1 lines
 set -o pipefail
 mkdir -p gpurun_out/r5b
 T="timeout -k 10"
-$T 900 python -u -m pytest tests/test_shard_gpu.py tests/test_cpp_dropin.py tests/test_gpu_keyrange.py tests/test_gpu_ref_full.py -x -v --timeout 300 --timeout-method thread -m gpu > gpurun_out/r5b/t.txt 2>&1 || exit 1
+$T 900 python -u -m pytest tests -x -v --timeout 300 --timeout-method thread -m gpu > gpurun_out/r5b/t.txt 2>&1 || exit 1
 for i in 1 2; do
   SRS_PAIR_TILES=0 $T 200 python -u bench.py --config c2 --steps 10 --cpu-sample 0 --extra none --alloc-steps 0 > gpurun_out/r5b/c2_off_$i.json 2>gpurun_out/r5b/c2_off_$i.err || exit 2
   $T 200 python -u bench.py --config c2 --steps 10 --cpu-sample 0 --extra none --alloc-steps 0 > gpurun_out/r5b/c2_on_$i.json 2>gpurun_out/r5b/c2_on_$i.err || exit 3
