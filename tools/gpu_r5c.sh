@@ -1,0 +1,7 @@
+# round 5, GPU call c: the default bench line (driver's command), then the
+# round profile (kernel trace + HBM counter passes) of the headline
+set -o pipefail
+mkdir -p gpurun_out/r5c
+T="timeout -k 10"
+/usr/bin/time -v $T 600 python -u bench.py > gpurun_out/r5c/bench_default.json 2> gpurun_out/r5c/bench_default.err || exit 1
+bash tools/profile_round.sh r05 --cpu-sample 0 --alloc-steps 0 --steps 10 > gpurun_out/r5c/prof.log 2>&1 || exit 2

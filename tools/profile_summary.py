@@ -32,7 +32,8 @@ def short(name):
 def base_kernel(name):
     """scatter_kernel<...> -> scatter (the names bench.py reports)."""
     n = short(name).split("<")[0]
-    return {"scatter_kernel": "scatter", "count_kernel": "count", "local_kernel": "local_fast",
+    return {"scatter_kernel": "scatter", "scatter_pair_kernel": "scatter",
+            "count_kernel": "count", "local_kernel": "local_fast",
             "local_stable_kernel": "local_stable", "local_lsd_kernel": "local_lsd"}.get(n, n)
 
 
