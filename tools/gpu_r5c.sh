@@ -3,5 +3,7 @@
 set -o pipefail
 mkdir -p gpurun_out/r5c
 T="timeout -k 10"
-/usr/bin/time -v $T 600 python -u bench.py > gpurun_out/r5c/bench_default.json 2> gpurun_out/r5c/bench_default.err || exit 1
+t0=$(date +%s)
+$T 600 python -u bench.py > gpurun_out/r5c/bench_default.json 2> gpurun_out/r5c/bench_default.err || exit 1
+echo "bench wall s: $(( $(date +%s) - t0 ))" > gpurun_out/r5c/bench_wall.txt
 bash tools/profile_round.sh r05 --cpu-sample 0 --alloc-steps 0 --steps 10 > gpurun_out/r5c/prof.log 2>&1 || exit 2
