@@ -7,5 +7,9 @@ for i in 1 2; do
   SRS_PAIR_TILES=0 $T 200 python -u bench.py --config c2 --steps 10 --cpu-sample 0 --extra none --alloc-steps 0 > gpurun_out/r5b/c2_off_$i.json 2>gpurun_out/r5b/c2_off_$i.err || exit 2
   $T 200 python -u bench.py --config c2 --steps 10 --cpu-sample 0 --extra none --alloc-steps 0 > gpurun_out/r5b/c2_on_$i.json 2>gpurun_out/r5b/c2_on_$i.err || exit 3
 done
+for i in 1 2; do
+  $T 200 python -u bench.py --config c1 --steps 10 --cpu-sample 0 --extra none --alloc-steps 0 > gpurun_out/r5b/c1_def_$i.json 2>gpurun_out/r5b/c1_def_$i.err || exit 6
+  SRS_PAIR_TILES=1 $T 200 python -u bench.py --config c1 --steps 10 --cpu-sample 0 --extra none --alloc-steps 0 > gpurun_out/r5b/c1_pair_$i.json 2>gpurun_out/r5b/c1_pair_$i.err || exit 7
+done
 $T 300 python -u bench.py --shard --steps 5 --warmup 1 --cpu-sample 0 --extra none --alloc-steps 0 > gpurun_out/r5b/shard_w1_default.json 2> gpurun_out/r5b/shard_w1_default.err || exit 4
 $T 300 python -u bench.py --shard --steps 5 --warmup 1 --cpu-sample 0 --extra none --alloc-steps 0 --rounds 16 --chunks 8 > gpurun_out/r5b/shard_w1_r16c8.json 2> gpurun_out/r5b/shard_w1_r16c8.err || exit 5
