@@ -956,3 +956,35 @@ def test_placed_device_memory():
     assert srs_amd.debug_probe_write(big.data_ptr(), 8 << 28) > 0
     del big, ko, po
     torch.cuda.synchronize()
+
+
+@pytest.mark.parametrize("shape", ["u64_u64", "u32_u32", "u32_keys", "f64_u64", "aos16"])
+def test_tile_pair_scatter_all_shapes(shape, monkeypatch):
+    """The tile-pair scatter (two count tiles per workgroup)
+    forced onto every shape it accepts (SRS_PAIR_TILES=1: the key plus one
+    column of 4- and 8-byte keys, AoS slices): stable, bit for bit, over
+    sizes whose levels have pairs that straddle two segments."""
+    torch = _torch()
+    monkeypatch.setenv("SRS_PAIR_TILES", "1")
+    for n in (70_001, 1_234_567):
+        for dist in ("uniform", "gaussian"):
+            if shape == "aos16":
+                keys = make_keys(6, dist, n, n % 97)
+                rec = np.empty((n, 16), np.uint8)
+                rec[:, :8] = keys.view(np.uint8).reshape(n, 8)
+                rec[:, 8:] = np.arange(n, dtype=np.uint64).view(np.uint8).reshape(n, 8)
+                d = torch.from_numpy(rec.copy()).cuda()
+                srs_amd.sort_combined_device(d, 6)
+                torch.cuda.synchronize()
+                assert bytes_equal(d.cpu().numpy(), stable_aos(6, True, rec)), (shape, n, dist)
+                continue
+            kind = {"u64_u64": 6, "u32_u32": 4, "u32_keys": 4, "f64_u64": 9}[shape]
+            keys = make_keys(kind, dist, n, n % 89)
+            cols = [keys]
+            if shape != "u32_keys":
+                cols.append(np.arange(n, dtype=np.uint64 if kind in (6, 9) else np.uint32))
+            host = [c.copy() for c in cols]
+            srs_amd.sort(*host)
+            st = stable_reference(kind, True, cols)
+            for a, b in zip(host, st):
+                assert bytes_equal(a, b), (shape, n, dist)
