@@ -514,11 +514,15 @@ def measure(cfg_name, args, torch, srs_amd, dist, dev, rank, world, shard):
     ms_no_events = (time.perf_counter() - t2) / nb * 1e3
     phases = None
     if shard:
-        # per-rank phase stamps of the last step (HIP events), the bytes each
-        # rank sent to each peer, the implied link rate and the DESIGN.md §7
-        # model's prediction for those bytes
-        mine = sorter.phases()
-        mine["rank"] = rank
+        # per-rank phase stamps of the last step (HIP events, from the
+        # library's report), the bytes each rank sent to each peer, the
+        # implied link rate, the non-overlapped head and tail and the
+        # DESIGN.md §7 model's prediction
+        rep = comm.report()
+        mine = {"rank": rank, "chunks": rep["chunks"], "rounds": rep["rounds"],
+                "stamps_ms": rep["stamps_ms"],
+                "bytes_to_peer_per_round": rep["bytes_to_peer_per_round"],
+                **shard_mod.link_figures(rep)}
         if world == 1:
             # the head and tail measured here, in DESIGN.md §7's 8-GPU model
             # (T(1) = the plain one-GPU step of the same shape, 21.2 ms for C1
@@ -529,6 +533,10 @@ def measure(cfg_name, args, torch, srs_amd, dist, dev, rank, world, shard):
         allph = [None] * world
         dist.all_gather_object(allph, mine)
         phases = allph
+    alloc_ms = {}
+    if not shard and args.alloc_steps > 0:
+        alloc_ms = alloc_variants(args, step_args=(keys, pays, rec, kind, layout), torch=torch,
+                                  srs_amd=srs_amd)
     if shard:
         tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
