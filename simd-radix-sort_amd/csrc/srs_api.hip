@@ -1138,16 +1138,21 @@ int plan_balanced_level(Workspace* W, const Request& R, const SortDesc& d, bool*
   return SRS_OK;
 }
 
-// The tile-pair scatter (scatter_pair_kernel) takes the
-// shapes whose runs per tile are shortest: 4-byte keys with C2's pair word
-// (SRS_PAIR_TILES=0 turns it off, =1 also takes the key + one column shapes
-// of 4- and 8-byte keys, A/B runs).
-bool pair_tiles_ok(const SortDesc& d, int ks) {
+// The tile-pair scatter (scatter_pair_kernel): where it
+// pays. Returns 0 (the 4096-key scatter), 1 (pairs on plain-digit levels) or
+// 2 (pairs on every level it supports, the small digit tables included).
+// Default: 4-byte keys with C2's pair word, plain-digit levels (measured:
+// C2's second level 5.35 -> 4.96 ms per launch, its digit-table first level
+// 5.24 -> 5.88). SRS_PAIR_TILES (A/B runs): 0 off, 1 also the key + one
+// column shapes of 4- and 8-byte keys, 3 every supported shape and level.
+int pair_tiles_mode(const SortDesc& d, int ks) {
   const char* e = getenv("SRS_PAIR_TILES");
   const int mode = e && *e ? atoi(e) : 2;
-  if (mode == 0 || d.canon_zero || (ks != 4 && ks != 8)) return false;
-  if (d.pair) return ks == 4 && d.ncols == 3;
-  return mode == 1 && d.ncols <= 2;
+  if (mode == 0 || d.canon_zero || (ks != 4 && ks != 8)) return 0;
+  const bool shape = d.pair ? ks == 4 && d.ncols == 3 : d.ncols <= 2;
+  if (!shape) return 0;
+  if (mode == 3) return 2;
+  return (d.pair || mode == 1) ? 1 : 0;
 }
 
 struct LevelState {
@@ -1156,7 +1161,7 @@ struct LevelState {
   int ncols;               // columns moved with the keys (SortDesc::ncols)
   int tmp2;                // SortDesc::tmp2
   int64_t known_len = -1;  // the length of the single big segment, when the host knows it
-  int pair_tiles = 0;      // the scatter takes two count tiles per workgroup (pair_tiles_ok)
+  int pair_tiles = 0;      // the scatter takes two count tiles per workgroup (pair_tiles_mode)
   int level = 0;           // global levels run so far (per-level timing names)
 };
 
@@ -1276,7 +1281,7 @@ int run_level(Workspace* W, int ks, const SortDesc* d_desc, LevelState& S, int f
     HIP_TRY(hipMemsetAsync(g_lb_status, 0, (size_t)ntiles * kMaxBins * 4, st));
   {
     TimedScope ts("scatter", (double)0, st, lv);
-    if (S.pair_tiles && lut != 1)
+    if ((S.pair_tiles == 1 && lut == 0) || (S.pair_tiles == 2 && lut != 1))
       launch_scatter_pairs(ks, d_desc, plan, tile_seg, (uint64_t*)W->offs.p,
                            offs32 ? (const uint32_t*)W->offs.p : nullptr, ntiles, lut, st, M.gt);
     else
@@ -1691,7 +1696,7 @@ int run_sort(Workspace* W, const Request& R, hipStream_t st) {
     W->h_ctr->local_elems = to_local ? (uint64_t)n : 0;
   }
   LevelState S{n_big, n_local, n_local2, n_copy, 0, d.ncols, d.tmp2};
-  S.pair_tiles = pair_tiles_ok(d, ks) ? 1 : 0;
+  S.pair_tiles = pair_tiles_mode(d, ks);
   if (R.nsegs == 0 && n_big == 1) S.known_len = n;
   int level = 0;
   // Stripe first level: large plain SoA sorts partition

@@ -958,14 +958,15 @@ def test_placed_device_memory():
     torch.cuda.synchronize()
 
 
+@pytest.mark.parametrize("mode", ["1", "3"])
 @pytest.mark.parametrize("shape", ["u64_u64", "u32_u32", "u32_keys", "f64_u64", "aos16"])
-def test_tile_pair_scatter_all_shapes(shape, monkeypatch):
+def test_tile_pair_scatter_all_shapes(shape, mode, monkeypatch):
     """The tile-pair scatter (two count tiles per workgroup)
-    forced onto every shape it accepts (SRS_PAIR_TILES=1: the key plus one
+    forced onto every shape it accepts (SRS_PAIR_TILES=1 / 3: the key plus one
     column of 4- and 8-byte keys, AoS slices): stable, bit for bit, over
     sizes whose levels have pairs that straddle two segments."""
     torch = _torch()
-    monkeypatch.setenv("SRS_PAIR_TILES", "1")
+    monkeypatch.setenv("SRS_PAIR_TILES", mode)
     for n in (70_001, 1_234_567):
         for dist in ("uniform", "gaussian"):
             if shape == "aos16":
@@ -988,3 +989,22 @@ def test_tile_pair_scatter_all_shapes(shape, monkeypatch):
             st = stable_reference(kind, True, cols)
             for a, b in zip(host, st):
                 assert bytes_equal(a, b), (shape, n, dist)
+
+
+def test_tile_pair_scatter_on_the_digit_table_level(monkeypatch):
+    """C2's shape at 2^24 + 4321 keys (a balanced digit-table first level)
+    with the tile-pair scatter on every level (SRS_PAIR_TILES=3), index
+    payloads: stable, bit for bit."""
+    torch = _torch()
+    monkeypatch.setenv("SRS_PAIR_TILES", "3")
+    n = (1 << 24) + 4321
+    keys = torch.empty(n, dtype=torch.float32, device="cuda")
+    p0 = torch.empty(n, dtype=torch.int32, device="cuda")
+    srs_amd.fill_synthetic_device(keys, p0)
+    p1 = torch.arange(n, dtype=torch.int32, device="cuda")
+    kh, ah, bh = keys.cpu().numpy(), p0.cpu().numpy(), p1.cpu().numpy()
+    srs_amd.sort_device(keys, p0, p1)
+    torch.cuda.synchronize()
+    st = stable_reference(8, True, [kh, ah, bh])
+    assert bytes_equal(keys.cpu().numpy(), st[0])
+    assert bytes_equal(p0.cpu().numpy(), st[1]) and bytes_equal(p1.cpu().numpy(), st[2])
