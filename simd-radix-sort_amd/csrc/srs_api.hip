@@ -1139,20 +1139,25 @@ int plan_balanced_level(Workspace* W, const Request& R, const SortDesc& d, bool*
 }
 
 // The tile-pair scatter (scatter_pair_kernel): where it
-// pays. Returns 0 (the 4096-key scatter), 1 (pairs on plain-digit levels) or
-// 2 (pairs on every level it supports, the small digit tables included).
-// Default: 4-byte keys with C2's pair word, plain-digit levels (measured:
-// C2's second level 5.35 -> 4.96 ms per launch, its digit-table first level
-// 5.24 -> 5.88). SRS_PAIR_TILES (A/B runs): 0 off, 1 also the key + one
-// column shapes of 4- and 8-byte keys, 3 every supported shape and level.
+// pays, as flags: 1 on plain-digit levels, 2 also on small-digit-table
+// levels, 4 not on the first level. Measured in one process, arms
+// alternated (tools/ab_inproc.py, profiles/r05/): C1 21.34 -> 20.94 ms per
+// step (both levels), C2's plain second level 5.36 -> 4.98 ms per launch but
+// its digit-table first level 5.18 -> 5.89, C3's second level 6.21 -> 5.98
+// but its first (whole 16-byte records read with a stride) 6.14 -> 6.31.
+// Default: plain-digit levels, AoS records from the second level on.
+// SRS_PAIR_TILES (A/B runs): 0 off, 1 every plain-digit level, 3 every
+// supported level, 2 (or unset) the default.
 int pair_tiles_mode(const SortDesc& d, int ks) {
   const char* e = getenv("SRS_PAIR_TILES");
   const int mode = e && *e ? atoi(e) : 2;
   if (mode == 0 || d.canon_zero || (ks != 4 && ks != 8)) return 0;
   const bool shape = d.pair ? ks == 4 && d.ncols == 3 : d.ncols <= 2;
   if (!shape) return 0;
-  if (mode == 3) return 2;
-  return (d.pair || mode == 1) ? 1 : 0;
+  if (mode == 3) return 1 | 2;
+  if (mode == 1) return 1;
+  const bool aos_slices = d.tmp2 && !d.pair;
+  return aos_slices ? (1 | 4) : 1;
 }
 
 struct LevelState {
@@ -1281,7 +1286,9 @@ int run_level(Workspace* W, int ks, const SortDesc* d_desc, LevelState& S, int f
     HIP_TRY(hipMemsetAsync(g_lb_status, 0, (size_t)ntiles * kMaxBins * 4, st));
   {
     TimedScope ts("scatter", (double)0, st, lv);
-    if ((S.pair_tiles == 1 && lut == 0) || (S.pair_tiles == 2 && lut != 1))
+    const bool pairs = (S.pair_tiles & 1) && (lut == 0 || ((S.pair_tiles & 2) && lut == 2)) &&
+                       !((S.pair_tiles & 4) && lv == 1);
+    if (pairs)
       launch_scatter_pairs(ks, d_desc, plan, tile_seg, (uint64_t*)W->offs.p,
                            offs32 ? (const uint32_t*)W->offs.p : nullptr, ntiles, lut, st, M.gt);
     else
