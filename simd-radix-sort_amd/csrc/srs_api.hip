@@ -1152,7 +1152,10 @@ int pair_tiles_mode(const SortDesc& d, int ks) {
   const char* e = getenv("SRS_PAIR_TILES");
   const int mode = e && *e ? atoi(e) : 2;
   if (mode == 0 || d.canon_zero || (ks != 4 && ks != 8)) return 0;
-  const bool shape = d.pair ? ks == 4 && d.ncols == 3 : d.ncols <= 2;
+  // (the kernel holds column 0 in a register of the key's width: an AoS
+  // record wider than its key, e.g. DataElement<float, uint32>, is not for it)
+  const bool shape = d.cols[0].width == (uint32_t)ks &&
+                     (d.pair ? ks == 4 && d.ncols == 3 : d.ncols <= 2);
   if (!shape) return 0;
   if (mode == 3) return 1 | 2;
   if (mode == 1) return 1;

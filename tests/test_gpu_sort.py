@@ -959,7 +959,8 @@ def test_placed_device_memory():
 
 
 @pytest.mark.parametrize("mode", ["1", "3"])
-@pytest.mark.parametrize("shape", ["u64_u64", "u32_u32", "u32_keys", "f64_u64", "aos16"])
+@pytest.mark.parametrize("shape", ["u64_u64", "u32_u32", "u32_keys", "f64_u64", "aos16",
+                                   "aos8_f32"])
 def test_tile_pair_scatter_all_shapes(shape, mode, monkeypatch):
     """The tile-pair scatter (two count tiles per workgroup)
     forced onto every shape it accepts (SRS_PAIR_TILES=1 / 3: the key plus one
@@ -969,6 +970,16 @@ def test_tile_pair_scatter_all_shapes(shape, mode, monkeypatch):
     monkeypatch.setenv("SRS_PAIR_TILES", mode)
     for n in (70_001, 1_234_567):
         for dist in ("uniform", "gaussian"):
+            if shape == "aos8_f32":  # DataElement<float, uint32>: record wider than its key
+                keys = make_keys(8, dist, n, n % 83)
+                rec = np.empty((n, 8), np.uint8)
+                rec[:, :4] = keys.view(np.uint8).reshape(n, 4)
+                rec[:, 4:] = np.arange(n, dtype=np.uint32).view(np.uint8).reshape(n, 4)
+                d = torch.from_numpy(rec.copy()).cuda()
+                srs_amd.sort_combined_device(d, 8)
+                torch.cuda.synchronize()
+                assert bytes_equal(d.cpu().numpy(), stable_aos(8, True, rec)), (shape, n, dist)
+                continue
             if shape == "aos16":
                 keys = make_keys(6, dist, n, n % 97)
                 rec = np.empty((n, 16), np.uint8)
