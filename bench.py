@@ -157,6 +157,13 @@ def pmc_traffic(kernel, workload, n):
     return best
 
 
+def progress(msg):
+    """A progress line on stderr (the JSON line stays alone on stdout): the
+    full-config CPU baselines run for minutes, and a run that prints nothing
+    for that long looks hung to a watchdog."""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def kind_id(name):
     import srs_amd
     return {"u64": srs_amd.KEY_U64, "f32": srs_amd.KEY_F32, "u32": srs_amd.KEY_U32}[name]
@@ -235,13 +242,16 @@ def cpu_baseline(cfg_name, n_sample, warmups=1):
             ns = (time.process_time() - c0) * 1e9
         return time.perf_counter() - t0, ns
 
+    progress(f"cpu baseline {cfg_name}: {n} keys generated in {gen_s:.1f} s")
     warm = []
     for w in range(warmups):
         if w:
             host_workload(cfg_name, n, (43 + w) << 32, keys, pays)
         warm.append(round(one_sort(keys, pays)[0], 2))
+        progress(f"cpu baseline {cfg_name}: warmup sort {w + 1} took {warm[-1]} s")
     host_workload(cfg_name, n, 42 << 32, keys, pays)  # the timed data: the bench's own input
     dt, cpu_ns = one_sort(keys, pays)
+    progress(f"cpu baseline {cfg_name}: timed sort {dt:.1f} s wall")
     del keys, pays
     try:
         model = [l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo")
@@ -401,6 +411,8 @@ def measure(cfg_name, args, torch, srs_amd, dist, dev, rank, world, shard):
     kname, psizes, layout, cdesc = CONFIGS[cfg_name]
     kind = kind_id(kname)
     n = int(args.n)
+    if rank == 0:
+        progress(f"{cfg_name}: generating {n} records per GPU")
 
     tdt = {8: torch.int64, 4: torch.int32}
     key_dt = {"u64": torch.int64, "f32": torch.float32, "u32": torch.int32}[kname]
@@ -478,6 +490,8 @@ def measure(cfg_name, args, torch, srs_amd, dist, dev, rank, world, shard):
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
+    if rank == 0:
+        progress(f"{cfg_name}: warmup done, timing {args.steps} steps")
     srs_amd.reset_kernel_stats()
     # The timed steps carry HIP event markers around the scatter launches
     # only (async stream packets, no host waits): the roofline's launch
@@ -580,6 +594,8 @@ def measure(cfg_name, args, torch, srs_amd, dist, dev, rank, world, shard):
         pass_model["frac_of_8TBs_levels_run"] = round(
             b_run / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBS, 4)
 
+    if rank == 0:
+        progress(f"{cfg_name}: {ms_per_step:.3f} ms per step; verifying")
     verified = None
     if not args.no_verify and not shard:
         if layout == "aos":
