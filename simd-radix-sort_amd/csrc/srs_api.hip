@@ -348,10 +348,14 @@ hipError_t big_free(void* p, int mode) {
 constexpr size_t kPlaceMinBytes = size_t(256) << 20;
 constexpr int kPlaceTries = 4;
 // One placement at a time per device (probes of two buffers on one device
-// would time each other). Nothing here waits for other work on the device:
-// the probe runs on a private stream and touches only the new buffer, so a
-// thread that allocates while its device holds queued peer receives (the
-// multi-GPU shard, one host thread per GPU) never waits for another thread.
+// would time each other). The probe waits for the device to be idle (work
+// still running would time the probe, not the placement: a probe beside the
+// bench's input fill picked slow buffers, 22.4 vs 21.2 ms per C1 step) and
+// runs on a private stream; the lock is per device, so a thread placing a
+// buffer on its GPU never blocks another GPU's thread (a global
+// lock held across that wait could deadlock one-process multi-GPU sorts
+// whose peers' receives were queued behind it), and the shard reserves its
+// buffers before its first message.
 std::mutex g_plmu_map;                       // the map below
 std::map<int, std::unique_ptr<std::mutex>> g_plmu;
 std::mutex g_place_ref_mu;
@@ -375,6 +379,8 @@ hipError_t placed_alloc(void** p, size_t bytes, int mode) {
   hipError_t e = hipGetDevice(&dev);
   if (e != hipSuccess) return e;
   std::lock_guard<std::mutex> g(device_place_mutex(dev));
+  e = hipDeviceSynchronize();
+  if (e != hipSuccess) return e;
   hipStream_t ps = nullptr;
   e = hipStreamCreateWithFlags(&ps, hipStreamNonBlocking);
   if (e != hipSuccess) return e;
