@@ -298,7 +298,7 @@ int srs_set_host_devices(int32_t num_devices, const int32_t* devices);
  * sort will write (out-of-place outputs, in-place arrays). The scatter's
  * write rate depends on where a buffer sits in HBM (the same
  * kernel writes some allocations ~13 % slower); buffers of 256 MB and more
- * are probed with the sort's write pattern and re-placed (up to 4 tries,
+ * are probed with the sort's write pattern and re-placed (up to 6 tries,
  * while free memory allows) when slower than the fastest placement seen.
  * The sort's own workspace is placed the same way. SRS_PLACE=0 turns the
  * probing off. srs_free_device releases it. No counterpart in the
