@@ -351,6 +351,10 @@ constexpr size_t kPlaceMinBytes = size_t(256) << 20;
 // round 4's 1.12 let the latter through)
 constexpr int kPlaceTries = 6;
 constexpr double kPlaceSlack = 1.04;
+// before any buffer of the process has been probed: the fast class's probe
+// rate on MI355X (0.187-0.202 ms per GB in round 5's runs; the slow class
+// 0.22-0.25), so that the first buffer is held to the same bar
+constexpr double kPlaceFirstRef = 0.200;
 // One placement at a time per device (probes of two buffers on one device
 // would time each other). The probe waits for the device to be idle (work
 // still running would time the probe, not the placement: a probe beside the
@@ -420,9 +424,7 @@ hipError_t placed_alloc(void** p, size_t bytes, int mode) {
       rejected.push_back(c);
     }
     if (best_rate <= 0) break;  // (no probe possible: keep it)
-    if (ref > 0 ? best_rate <= kPlaceSlack * ref
-                : k > 0 && best_rate <= kPlaceSlack * seen)  // (first buffer: two looks)
-      break;
+    if (best_rate <= kPlaceSlack * (ref > 0 ? ref : kPlaceFirstRef)) break;
   }
   {
     std::lock_guard<std::mutex> r(g_place_ref_mu);
