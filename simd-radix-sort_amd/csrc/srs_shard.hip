@@ -453,6 +453,20 @@ std::vector<int32_t> balanced_split(const uint64_t* h, int nbins, int parts) {
   return out;
 }
 
+// Input chunk c of n records (of CH) starts at chunk_bound(n, c, CH): the
+// first chunk weighs 1, every other 4, so the first partition (which every
+// message waits for) is short. Rounds follow the same idea at the other end:
+// the last round weighs 1, the others 4, so the last round's sort (which
+// nothing overlaps) is short (head and tail).
+int64_t weighted_bound(int64_t m, int i, int parts, bool first_small) {
+  if (i <= 0) return 0;
+  if (i >= parts) return m;
+  const int64_t tot = 4 * (int64_t)parts - 3;
+  const int64_t w = first_small ? 4 * (int64_t)i - 3 : 4 * (int64_t)i;
+  return (int64_t)((__int128)m * w / tot);
+}
+int64_t chunk_bound(int64_t n, int c, int CH) { return weighted_bound(n, c, CH, true); }
+
 struct Msg {
   int op;        // 0 send, 1 receive, 2 own piece (a device copy)
   int peer;
@@ -509,9 +523,9 @@ struct ShardPlan {
   int64_t M(int src, int c, int g) const { return mat[((size_t)src * CH + c) * G + g]; }
   // round r of rank d: groups owned[d][lo, hi)
   void rgrp(int d, int r, int* lo, int* hi) const {
-    const int m = (int)owned[d].size();
-    *lo = (int)((int64_t)r * m / R);
-    *hi = (int)((int64_t)(r + 1) * m / R);
+    const int64_t m = (int64_t)owned[d].size();
+    *lo = (int)weighted_bound(m, r, R, false);
+    *hi = (int)weighted_bound(m, r + 1, R, false);
   }
   // (first group, records) of the round-r piece source `src` holds for rank
   // d in chunk c: a contiguous run of groups, so one range of its buffer
@@ -526,7 +540,7 @@ struct ShardPlan {
   void layout(const int64_t* all, int64_t n) {
     mat.assign(all, all + (size_t)w * CH * G);
     cb.resize(CH + 1);
-    for (int c = 0; c <= CH; c++) cb[c] = n * c / CH;
+    for (int c = 0; c <= CH; c++) cb[c] = chunk_bound(n, c, CH);
     // receive layout: round-major, then source, then chunk
     roff.assign((size_t)R * w * CH, 0);
     rb0.assign(R, 0);
@@ -762,7 +776,7 @@ int shard_sort(srs_shard_comm C, int64_t n, int kind, int up, const void* keys, 
   const int nb = P.nb, G = P.G;
   if (err) n = 0;
   std::vector<int64_t> cb(CH + 1);
-  for (int c = 0; c <= CH; c++) cb[c] = n * c / CH;
+  for (int c = 0; c <= CH; c++) cb[c] = chunk_bound(n, c, CH);
   C->clk.reset();
   C->clk.stamp("start", st);
 

@@ -40,12 +40,22 @@ def _top(kind, keys, bits):
         np.int64)
 
 
+def _chunk_bound(n, c, chunks):
+    """The library's chunk bounds (srs_shard.hip chunk_bound): the first
+    chunk weighs 1, every other 4."""
+    if c <= 0:
+        return 0
+    if c >= chunks:
+        return n
+    return n * (4 * c - 3) // (4 * chunks - 3)
+
+
 def _chunk_hists(kind, keys, chunks, bits):
     n = len(keys)
     out = np.zeros((chunks, 1 << bits), np.uint64)
     top = _top(kind, keys, bits)
     for c in range(chunks):
-        a, b = n * c // chunks, n * (c + 1) // chunks
+        a, b = _chunk_bound(n, c, chunks), _chunk_bound(n, c + 1, chunks)
         out[c] = np.bincount(top[a:b], minlength=1 << bits)
     return out
 
@@ -80,6 +90,7 @@ def _run_rank(rank, world, kind, dist_kind, n_per, chunks, rounds):
     kcol = keys.view(KIND_UINT[kind]).astype(np.int64)  # bits, widened for gloo
     part_k, part_p = np.empty_like(kcol), np.empty_like(pay)
     cbnd = plan["chunk_bounds"]
+    assert cbnd == [_chunk_bound(n, c, chunks) for c in range(chunks + 1)]
     for c in range(chunks):
         a, b = cbnd[c], cbnd[c + 1]
         order = a + np.argsort(gob[top[a:b]], kind="stable")
@@ -215,7 +226,7 @@ def test_shard_plan_messages_pair_up(world, chunks, rounds, kind):
     for s in range(world):
         top = np.minimum(rng.geometric(0.002, ns[s]) - 1, nb - 1)  # skewed bins
         for c in range(chunks):
-            a, b = ns[s] * c // chunks, ns[s] * (c + 1) // chunks
+            a, b = _chunk_bound(ns[s], c, chunks), _chunk_bound(ns[s], c + 1, chunks)
             hs[s, c] = np.bincount(top[a:b], minlength=nb)
     plans = [shard.debug_plan(world, r, chunks, rounds, kbits, hs, ns[r]) for r in range(world)]
     assert all(p["group_of_bin"] == plans[0]["group_of_bin"] for p in plans)
@@ -250,3 +261,20 @@ def test_shard_plan_messages_pair_up(world, chunks, rounds, kind):
             assert x["bounds"][0] == 0 and x["bounds"][-1] == x["end"] - x["start"] or \
                 x["end"] == x["start"]
             assert 0 <= x["known_bits"] < kbits
+
+
+def test_shard_plan_small_first_chunk_and_last_round():
+    """The head and tail of the exchange: with uniform keys the
+    first partition chunk and the last round are the short ones (weight 1
+    against 4)."""
+    shard = _shard()
+    world, chunks, rounds, n = 8, 8, 16, 1 << 20
+    rng = np.random.default_rng(3)
+    keys = rng.integers(0, 2**63, n, dtype=np.uint64) << np.uint64(1)
+    hs = np.stack([_chunk_hists(6, keys, chunks, 12)] * world)
+    p = shard.debug_plan(world, 0, chunks, rounds, 64, hs, n)
+    cb = p["chunk_bounds"]
+    sizes = [b - a for a, b in zip(cb[:-1], cb[1:])]
+    assert sizes[0] * 3 < min(sizes[1:]), sizes
+    rs = [x["end"] - x["start"] for x in p["rounds"]]
+    assert rs[-1] < 0.6 * min(rs[:-1]), rs  # (whole groups: 2 of rank 0's 64 against 4-5)
