@@ -269,11 +269,11 @@ int srs_shard_debug_inject(srs_shard_comm comm, int32_t point);
  * histograms (chunk_hists[src][chunk][2^min(12, key_bits)] of the
  * transformed top key bits) and this rank's record count, the JSON of
  * group_of_bin, rank_of_group, chunk_bounds, total (records received),
- * "posts" (every message group in posting order: round, chunks, msgs =
- * [op (0 send, 1 receive, 2 own-piece copy), peer, partitioned offset,
- * receive offset, records]) and "rounds" (each round's receive range, its
- * sort segments and known top bits). The same code plans the device sort;
- * tests drive the protocol with it on CPU (gloo). */
+ * "posts" (every message group in posting order: its (round, chunk) pieces
+ * and msgs = [op (0 send, 1 receive, 2 own-piece copy), peer, partitioned
+ * offset, receive offset, records]) and "rounds" (each round's receive
+ * range, its sort segments and known top bits). The same code plans the
+ * device sort; tests drive the protocol with it on CPU (gloo). */
 int srs_debug_shard_plan(int32_t world, int32_t rank, int32_t chunks, int32_t rounds,
                          int32_t key_bits, const uint64_t* chunk_hists, int64_t num, char* json,
                          int64_t cap);
