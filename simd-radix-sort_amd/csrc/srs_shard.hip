@@ -143,7 +143,8 @@ constexpr int kGroups = 512;                     // key-range groups
 constexpr int kMaxChunks = 16;                   // partition chunks
 constexpr int kMaxRounds = 64;                   // exchange rounds
 constexpr int kDefaultChunks = 8;                // (world > 1; world 1: one chunk)
-constexpr int kDefaultRounds = 8;
+constexpr int kDefaultRounds = 16;               // (world > 1; world 1: 8)
+constexpr int kDefaultRounds1 = 8;
 constexpr int kHdr = 16;                         // header slots after the histogram
 constexpr size_t kMsgBytes = size_t(256) << 20;  // largest message
 
@@ -782,7 +783,7 @@ int shard_sort(srs_shard_comm C, int64_t n, int kind, int up, const void* keys, 
   const int ks = err ? 8 : key_bytes(kind);
   const int kbits = 8 * ks;
   const int CH = C->chunks > 0 ? C->chunks : (w > 1 ? kDefaultChunks : 1);
-  const int R = C->rounds > 0 ? C->rounds : kDefaultRounds;
+  const int R = C->rounds > 0 ? C->rounds : (w > 1 ? kDefaultRounds : kDefaultRounds1);
   const int ncols = 1 + np;
   std::vector<uint32_t> width(ncols);
   width[0] = (uint32_t)ks;
