@@ -179,17 +179,21 @@ def _sm64(x, np):
     return x ^ (x >> np.uint64(31))
 
 
-def host_workload(cfg_name, n, seed, keys=None, pays=None, chunk=1 << 26):
+def host_workload(cfg_name, n, seed, keys=None, pays=None, chunk=1 << 24, threads=8):
     """The config's records on the host, by the device fill's generator
     (srs_fill_synthetic_device: key = splitmix64(seed + i), payload c =
     splitmix64(bits(key) ^ c * 0xD1B54A32D192ED03)), generated chunk by chunk
-    into `keys` / `pays` (allocated when None)."""
+    into `keys` / `pays` (allocated when None), chunks on `threads` host
+    threads (numpy releases the GIL in its array loops; generation is not
+    timed, it only has to stay short)."""
     import numpy as np
+    from concurrent.futures import ThreadPoolExecutor
     kname, psizes, _, _ = CONFIGS[cfg_name]
     if keys is None:
         keys = np.empty(n, np.float32 if kname == "f32" else np.uint64)
         pays = [np.empty(n, {4: np.uint32, 8: np.uint64}[s]) for s in psizes]
-    for a in range(0, n, chunk):
+
+    def gen(a):
         b = min(n, a + chunk)
         h = _sm64(np.arange(a, b, dtype=np.uint64) + np.uint64(seed), np)
         if kname == "f32":
@@ -202,6 +206,8 @@ def host_workload(cfg_name, n, seed, keys=None, pays=None, chunk=1 << 26):
         for c, p in enumerate(pays):
             p[a:b] = _sm64(bits ^ np.uint64((c * 0xD1B54A32D192ED03) & 0xFFFFFFFFFFFFFFFF),
                            np).astype(p.dtype)
+    with ThreadPoolExecutor(max_workers=max(1, threads)) as ex:
+        list(ex.map(gen, range(0, n, chunk)))
     return keys, pays
 
 
