@@ -1716,9 +1716,10 @@ __global__ __launch_bounds__(kScatterThreads, SRS_SCATTER_WAVES_PER_EU) void sca
 // and adding tile a's offsets gives the same stable result. 512 threads x 16
 // records; the LDS holds one 8-byte slot per record (the 4-byte keys use
 // half of it), 8 per-wave counter rows and the bucket bases: 79 KB with the
-// small digit table, two workgroups per CU. Digits are recomputed from the
-// staged key instead of staged. Columns: the key plus one column, or the
-// key plus C2's pair word (SortDesc::pair).
+// small digit table, two workgroups per CU. 8-byte keys recompute each
+// slot's digit from the staged key; 4-byte keys stage it in the half of the
+// slot area they leave free. Columns: the key plus one column, or the key
+// plus C2's pair word (SortDesc::pair).
 constexpr int kPairThreads = 512;
 constexpr int kPairItems = 16;
 constexpr int kPairTile = 2 * kTile;
@@ -1837,12 +1838,17 @@ __device__ __forceinline__ void scatter_pair_tiles(
   }
   lds_barrier();
   KR* skey = (KR*)L.sval;
+  // 4-byte keys fill half of the slot area: the other half holds each slot's
+  // digit (no table lookup again at the stores; the word column overwrites
+  // both afterwards)
+  uint16_t* sdig = (uint16_t*)((char*)L.sval + (size_t)kPairTile * 4);
 #pragma unroll
   for (int k = 0; k < IT; k++)
     if (valid(k)) {
       const uint32_t d = dg[k];
       pos[k] = L.bin_start[d] + L.wc[wave][d] + pos[k];
       skey[pos[k]] = v0[k];
+      if constexpr (KW == 4) sdig[pos[k]] = (uint16_t)d;
     }
   lds_barrier();
   // the key column: slot j's bucket from its staged key
@@ -1857,7 +1863,9 @@ __device__ __forceinline__ void scatter_pair_tiles(
         dout[i] = 0;
         if (j < total) {
           const KR x = skey[j];
-          const uint32_t d = pass_digit<LUT>(xf((U)x & kmask), P.shift, mask, lut);
+          uint32_t d;
+          if constexpr (KW == 4) d = sdig[j];
+          else d = pass_digit<LUT>(xf((U)x & kmask), P.shift, mask, lut);
           dout[i] = (uint16_t)d;
           stw<decltype(W_)::value>(out + ((int64_t)j + L.gdst[d]) * (int64_t)st, (uint64_t)x);
         }
