@@ -1154,10 +1154,12 @@ int plan_balanced_level(Workspace* W, const Request& R, const SortDesc& d, bool*
 // pays, as flags: 1 on plain-digit levels, 2 also on small-digit-table
 // levels, 4 not on the first level. Measured in one process, arms
 // alternated (tools/ab_inproc.py, profiles/r05/): C1 21.34 -> 20.94 ms per
-// step (both levels), C2's plain second level 5.36 -> 4.98 ms per launch but
-// its digit-table first level 5.18 -> 5.89, C3's second level 6.21 -> 5.98
-// but its first (whole 16-byte records read with a stride) 6.14 -> 6.31.
-// Default: plain-digit levels, AoS records from the second level on.
+// step (both levels), C2 17.60 -> 16.92 (both levels, with the 4-byte keys'
+// digits staged: its digit-table first level 5.29 -> 4.99 ms per launch, the
+// plain second 5.42 -> 5.06; before the staging the table level lost, 5.18
+// -> 5.89), C3's second level 6.21 -> 5.98 but its first (whole 16-byte
+// records read with a stride) 6.14 -> 6.31. Default: plain-digit levels,
+// small digit tables with 4-byte keys, AoS records from the second level on.
 // SRS_PAIR_TILES (A/B runs): 0 off, 1 every plain-digit level, 3 every
 // supported level, 2 (or unset) the default.
 int pair_tiles_mode(const SortDesc& d, int ks) {
@@ -1172,7 +1174,7 @@ int pair_tiles_mode(const SortDesc& d, int ks) {
   if (mode == 3) return 1 | 2;
   if (mode == 1) return 1;
   const bool aos_slices = d.tmp2 && !d.pair;
-  return aos_slices ? (1 | 4) : 1;
+  return aos_slices ? (1 | 4) : ks == 4 ? (1 | 2) : 1;
 }
 
 struct LevelState {
