@@ -16,6 +16,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstring>
 #include <cstdio>
 #include <cstdlib>
@@ -486,8 +487,11 @@ struct Workspace {
   // second level's tile counts and gathered tile table (GTile)
   DevBuf prun, ptile, btot, bnt, btile, nt_over, gtile, gorder;
   int64_t gorder_cap = 0;
+  DevBuf mid;  // mid-size single launch: the tiles' key OR / AND, their digit counts
   ListCounters* h_ctr = nullptr;
   uint64_t* h_totals = nullptr;
+  MidFlag* h_mid = nullptr;        // the mid-size launch's early answer
+  unsigned long long mid_seq = 0;  // (its sequence numbers)
   // Stream order of the workspace: the last call's kernels may still be
   // queued on its stream when the call returns. `idle` is recorded on that
   // stream at the end of every call; the next call's stream waits for it
@@ -516,17 +520,21 @@ struct Workspace {
                       &fallback2, &redo, &redo2, &shist, &lut, &lut_rbits, &copy, &plan, &tcount,
                       &gcount, &tbase, &gbase, &var, &sbase, &tile_seg, &group_seg, &hist, &offs,
                       &gsum, &gofs, &scan_tmp, &totals, &ctr, &prun, &ptile, &btot, &bnt, &btile,
-                      &nt_over, &gtile, &gorder};
+                      &nt_over, &gtile, &gorder, &mid};
     for (DevBuf* b : bufs) free_buf(*b);
     for (auto& t : small_taken) free_buf(t.second);
     if (h_ctr) (void)hipHostFree(h_ctr);
     if (h_totals) (void)hipHostFree(h_totals);
+    if (h_mid) (void)hipHostFree(h_mid);
     (void)hipGetLastError();  // (release-time failures leave no sticky error behind)
   }
 };
 
 std::mutex g_wmu;  // the map below
-std::map<int, std::shared_ptr<Workspace>> g_ws;
+// (never destroyed: at process exit the HIP runtime -- or a profiler's tool
+// library -- may already be torn down, and ~Workspace would call into it;
+// a segfault after rocprofv3's finalisation. srs_release_workspace frees.)
+std::map<int, std::shared_ptr<Workspace>>& g_ws = *new std::map<int, std::shared_ptr<Workspace>>;
 
 // A workspace held for one call: the reference keeps it alive, the lock
 // (taken after the lookup, released first) makes the call its only user.
@@ -546,6 +554,9 @@ int get_ws_locked(std::shared_ptr<Workspace>* out) {
   auto w = std::make_shared<Workspace>();
   HIP_TRY(hipHostMalloc((void**)&w->h_ctr, sizeof(ListCounters), hipHostMallocDefault));
   HIP_TRY(hipHostMalloc((void**)&w->h_totals, 4 * sizeof(uint64_t), hipHostMallocDefault));
+  // (coherent: the mid-size kernel stores into it while the host polls)
+  HIP_TRY(hipHostMalloc((void**)&w->h_mid, sizeof(MidFlag), hipHostMallocCoherent));
+  memset(w->h_mid, 0, sizeof(MidFlag));
   g_ws[dev] = w;
   *out = w;
   return SRS_OK;
@@ -1579,6 +1590,32 @@ int plan_range_level(Workspace* W, const Request& R, const std::vector<KeyCluste
 
 int copy_through(const Request& R, hipStream_t st);
 
+// Mid-size sorts (kLocalCap < n <= kMidMaxKeys) take one cooperative launch
+// (launch_mid_sort); SRS_MID=0 sends them down the general path.
+bool mid_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("SRS_MID");
+    return !(e && *e == '0');
+  }();
+  return on;
+}
+
+// Waits for the mid-size kernel's MidFlag of call `seq`: a short poll, then
+// the stream (which also surfaces a kernel failure).
+int wait_mid_flag(const MidFlag* f, unsigned long long seq, hipStream_t st) {
+  auto seen = [&] { return __atomic_load_n(&f->seq, __ATOMIC_ACQUIRE) == seq; };
+  const auto t0 = std::chrono::steady_clock::now();
+  while (!seen()) {
+    if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(5)) {
+      HIP_TRY(hipStreamSynchronize(st));
+      if (!seen()) return fail(SRS_ERR_INTERNAL, "mid-size launch: no answer from the kernel");
+      break;
+    }
+    __builtin_ia32_pause();
+  }
+  return SRS_OK;
+}
+
 int run_sort(Workspace* W, const Request& R, hipStream_t st) {
   if (R.nsegs == 0 && R.num <= kLocalCap) return run_small(W, R, st);
   {
@@ -1598,19 +1635,21 @@ int run_sort(Workspace* W, const Request& R, hipStream_t st) {
   d.canon_zero = (is_float && n <= R.thresh) ? 1 : 0;
   d.leaf_skip = leaf_skip_of(R);
   const int ksl = ks | (d.canon_zero ? SRS_KS_CANON : 0);  // kernel dispatch key
+  // (the mid-size launch moves the columns as they are: no slices, no pairs)
+  const bool mid = R.nsegs == 0 && n > kLocalCap && n <= kMidMaxKeys && mid_enabled();
 
   // AoS records of 16+ bytes travel as SoA slice columns through the
   // workspace (TMP, TMP2) between the first scatter and the local pass: the
   // later count passes then read 8-byte keys instead of whole records and
   // the middle scatters move dense columns
-  const bool aos_cols = R.aos && R.elem_size >= 16 && n > kLocalCap && R.nsegs == 0;
+  const bool aos_cols = R.aos && R.elem_size >= 16 && n > kLocalCap && R.nsegs == 0 && !mid;
   // A key and two 4-byte payload columns (C2) travel with the payloads
   // interleaved as one 8-byte word per record through TMP / TMP2: the
   // scatters then write 64-byte runs of words instead of two columns of
   // 32-byte runs (the same bytes as one 8-byte payload column measured
   // 23.6 -> 21.1 ms at 1e9)
   const bool pair_cols = !R.aos && R.ncols == 3 && R.widths[1] == 4 && R.widths[2] == 4 &&
-                         n > kLocalCap && R.nsegs == 0;
+                         n > kLocalCap && R.nsegs == 0 && !mid;
   size_t tmp_bytes = 0, slice_bytes = 0;
   std::vector<size_t> tmp_off;
   if (R.aos) {
@@ -1709,6 +1748,39 @@ int run_sort(Workspace* W, const Request& R, hipStream_t st) {
     n_local = (int64_t)hl.size();
     n_local2 = (int64_t)hl2.size();
     W->h_ctr->local_elems = lel;
+  } else if (mid) {
+    // one cooperative launch: the first level and every bucket's local sort;
+    // buckets over kLocalCap (skewed keys) come back in the big list and
+    // continue on the general levels below
+    const int64_t G = (n + kTile - 1) / kTile;
+    SRS_TRY(ensure(W->mid, G * 16 + G * kMaxBins * sizeof(uint32_t)));
+    DevBuf& taken = W->small_taken[st];
+    SRS_TRY(ensure(taken, 2 * sizeof(int64_t)));
+    hipError_t e;
+    const unsigned long long seq = ++W->mid_seq;
+    {
+      note_elems("mid", (double)n);
+      TimedScope ts("mid", (double)0, st);
+      e = launch_mid_sort(ksl, d, n, home, (unsigned long long*)W->mid.p,
+                          (uint32_t*)((char*)W->mid.p + G * 16), d_ctr, (Seg*)W->big[0].p,
+                          (unsigned long long*)taken.p, W->h_mid, seq, st);
+    }
+    if (e != hipSuccess) return fail(SRS_ERR_HIP, std::string("mid-size launch: ") +
+                                                      hipGetErrorString(e));
+    // The kernel's workgroup 0 posts the big-bucket count to host memory once
+    // the first level's sizes are known (MidFlag): polled for a while (a
+    // stream sync's wake-up cost ~30 us per call), then waited for
+    SRS_TRY(wait_mid_flag(W->h_mid, seq, st));
+    const unsigned long long nb_flag = __atomic_load_n(&W->h_mid->n_big, __ATOMIC_ACQUIRE);
+    if (nb_flag >> 63) return fail(SRS_ERR_INTERNAL, "mid-size launch: more buckets than workgroups");
+    n_big = (int64_t)nb_flag;
+    if (n_big == 0) {
+      W->last_small = true;  // (srs_debug_last_fallbacks reads `taken`)
+      W->last_small_stream = st;
+      return SRS_OK;
+    }
+    launch_set_desc(d, d_desc, st);
+    W->h_ctr->local_elems = 0;
   } else {
     Seg seg0{0, n, d.key_bits, home};
     const bool to_local = n <= kLocalCap;
@@ -1721,7 +1793,7 @@ int run_sort(Workspace* W, const Request& R, hipStream_t st) {
   }
   LevelState S{n_big, n_local, n_local2, n_copy, 0, d.ncols, d.tmp2};
   S.pair_tiles = pair_tiles_mode(d, ks);
-  if (R.nsegs == 0 && n_big == 1) S.known_len = n;
+  if (R.nsegs == 0 && n_big == 1 && !mid) S.known_len = n;
   int level = 0;
   // Stripe first level: large plain SoA sorts partition
   // stripes of kStripeKeysPerBucket << b1 keys on their own with the first
@@ -2036,7 +2108,7 @@ struct HostStage {  // per device, kept between calls
 };
 using StageRef = std::shared_ptr<HostStage>;
 std::mutex g_smu;
-std::map<int, StageRef> g_stage;
+std::map<int, StageRef>& g_stage = *new std::map<int, StageRef>;  // (never destroyed: as g_ws)
 
 // (the calling thread's current device is `dev`). The caller holds the
 // returned reference for as long as it uses the stage, so

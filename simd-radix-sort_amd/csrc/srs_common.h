@@ -117,6 +117,14 @@ struct GTile {
 #endif
 constexpr int kStripeKeysPerBucket = SRS_STRIPE_KPB;
 
+// The mid-size launch's answer to the host (coherent pinned host memory):
+// written by workgroup 0 once the first level's bucket sizes are known, so
+// the host need not wait for the whole kernel (seq last, release).
+struct MidFlag {
+  unsigned long long n_big;  // buckets handed back to the general levels (bit 63: error)
+  unsigned long long seq;    // the call's sequence number
+};
+
 // Work-list counters (device), read back by the host once per level.
 struct ListCounters {
   unsigned long long n_big;    // segments for the next global level

@@ -15,6 +15,7 @@
 //
 // All kernels are integer byte movement (no MFMA); the roofline is HBM.
 // wave64 everywhere; __ballot returns 64-bit masks.
+#include <hip/hip_cooperative_groups.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -3358,6 +3359,277 @@ __global__ __launch_bounds__(kLocalThreads) void small_sort_kernel(const SortDes
 }
 
 // ---------------------------------------------------------------------------
+// mid-size sorts (kLocalCap < n <= kMidMaxTiles * kTile) in ONE launch
+// ---------------------------------------------------------------------------
+// Between one workgroup's small sort and the general path (a plan, a count,
+// three offset kernels and a scatter per level, then the local kernels:
+// about twelve dependent launches, ~85 us of GPU-side span at 8K-64K keys,
+// almost all of it launch gaps) one cooperative launch of G = ceil(n / 4096)
+// workgroups does it all, with grid barriers between the phases:
+//   1. every workgroup loads its tile and reduces the keys' OR / AND;
+//   2. the global varying bits give the digit (choose_bits, as a level
+//      would), each tile counts its digits;
+//   3. each tile's bucket offsets follow from the T x 2^bits counts (every
+//      workgroup scans them itself) and the tile is scattered, stably, to
+//      TMP (scatter_process_tile, the global levels' code);
+//   4. workgroup b sorts bucket b in LDS with the small sort's bodies (fast,
+//      stable, LSD) into OUT; a bucket larger than kLocalCap (skewed keys)
+//      goes to the big list for the host's general levels (ctr->n_big, read
+//      back once).
+// G = max(T tiles, 2^choose_bits(n, 64)) workgroups (<= 128 at kMidMaxKeys):
+// one bucket each, no loop -- a loop over buckets had the compiler hoist the
+// bodies' per-thread invariants out of it and spill 55 VGPRs. One
+// workgroup per CU (129 KB of LDS), so G must fit the chip for the
+// cooperative launch.
+constexpr int kMidMaxTiles = 64;  // n <= 262144
+constexpr int kMidMat = 8192;     // tiles x buckets (64 x 128 at kMidMaxKeys)
+static_assert(kMidMat % kScatterThreads == 0, "count matrix: whole rounds of loads");
+
+struct MidLevelLds {
+  ScatterLds<0> sc;
+  SegPlan plan;
+  unsigned long long wor[kScatterThreads / 64], wand[kScatterThreads / 64];
+  uint32_t hist[kMaxBins];
+  uint32_t mat[kMidMat];  // every tile's bucket counts (phase 3)
+};
+
+__device__ __forceinline__ void mid_tell_host(MidFlag* f, unsigned long long n_big,
+                                              unsigned long long seq) {
+  __hip_atomic_store(&f->n_big, n_big, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(&f->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+union MidLds {
+  SmallLds local;
+  MidLevelLds level;
+};
+
+template <typename KT, typename U, bool CZ>
+__global__ __launch_bounds__(kLocalThreads) void mid_sort_kernel(
+    const SortDesc d, int64_t n, int32_t src, unsigned long long* __restrict__ part,
+    uint32_t* __restrict__ hist, ListCounters* __restrict__ ctr, Seg* __restrict__ big,
+    unsigned long long* __restrict__ taken, MidFlag* __restrict__ flag, unsigned long long seq) {
+  static_assert(kLocalThreads == kScatterThreads, "the level phases use the scatter's shape");
+  namespace cg = cooperative_groups;
+  cg::grid_group grid = cg::this_grid();
+  __shared__ MidLds Ls;
+  __shared__ int64_t my_start;
+  __shared__ int32_t my_len;
+  const SortDesc* desc = &d;
+  constexpr int IT = kScatterItems;
+  const int G = (int)gridDim.x;
+  const int T = (int)((n + kTile - 1) / kTile);  // tiles (workgroups [0, T))
+  const int w = (int)blockIdx.x;
+  const bool has_tile = w < T;
+  const uint32_t wave = threadIdx.x >> 6, lane = lane_id();
+  const int64_t tbase = (int64_t)w * kTile;
+  const int cnt = has_tile ? (int)std::min<int64_t>(kTile, n - tbase) : 0;
+  const int ebase = (int)wave * IT * 64 + (int)lane;
+  const int ncols = desc->ncols;
+  Xform<U, CZ> xf;
+  xf.init(*desc);
+  const int kbytes = desc->key_bits >> 3;
+  const uint64_t kmask = kbytes == 8 ? ~0ull : ((1ull << (8 * kbytes)) - 1);
+  auto valid = [&](int k) -> bool { return ebase + k * 64 < cnt; };
+
+  // ---- 1. the tile in registers; the keys' OR / AND
+  uint64_t v0[IT], v1[IT], v2[IT];
+  if (has_tile) {
+    load_strip<IT>(v0, desc->cols[0].base[src], desc->cols[0].width, desc->cols[0].stride[src],
+                   tbase, ebase, cnt);
+    if (ncols > 1)
+      load_strip<IT>(v1, desc->cols[1].base[src], desc->cols[1].width,
+                     desc->cols[1].stride[src], tbase, ebase, cnt);
+    unsigned long long kor = 0, kand = ~0ull;
+#pragma unroll
+    for (int k = 0; k < IT; k++)
+      if (valid(k)) {
+        const unsigned long long u = (unsigned long long)xf((U)(v0[k] & kmask));
+        kor |= u;
+        kand &= u;
+      }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      kor |= __shfl_xor(kor, o, 64);
+      kand &= __shfl_xor(kand, o, 64);
+    }
+    if (lane == 0) {
+      Ls.level.wor[wave] = kor;
+      Ls.level.wand[wave] = kand;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      unsigned long long o = 0, a = ~0ull;
+      for (int i = 0; i < kScatterThreads / 64; i++) {
+        o |= Ls.level.wor[i];
+        a &= Ls.level.wand[i];
+      }
+      part[2 * w] = o;
+      part[2 * w + 1] = a;
+    }
+  }
+  if (w == 0 && threadIdx.x == 0) {  // (every counter: a skewed sort continues on the general path)
+    *ctr = ListCounters{};
+    taken[0] = taken[1] = 0;
+  }
+  grid.sync();
+
+  // ---- 2. the digit; this tile's counts
+  // (the T pairs in one round of loads: a loop over them paid a cross-XCD
+  // round trip per tile)
+  unsigned long long gor = 0, gand = ~0ull;
+  {
+    unsigned long long o = 0, a = ~0ull;
+    if (threadIdx.x < (uint32_t)T) {
+      o = part[2 * threadIdx.x];
+      a = part[2 * threadIdx.x + 1];
+    }
+#pragma unroll
+    for (int s = 32; s > 0; s >>= 1) {
+      o |= __shfl_xor(o, s, 64);
+      a &= __shfl_xor(a, s, 64);
+    }
+    __syncthreads();  // (phase 1's reads of wor / wand are over)
+    if (lane == 0) {
+      Ls.level.wor[wave] = o;
+      Ls.level.wand[wave] = a;
+    }
+    __syncthreads();
+    for (int i = 0; i < kScatterThreads / 64; i++) {
+      gor |= Ls.level.wor[i];
+      gand &= Ls.level.wand[i];
+    }
+  }
+  const unsigned long long var = gor ^ gand;
+  if (var == 0) {  // every key equal: the input is the output (stable)
+    if (w == 0 && threadIdx.x == 0) mid_tell_host(flag, 0, seq);
+    if (src != BUF_OUT && has_tile)
+      for (int c = 0; c < ncols; c++) {
+        uint64_t t[IT];
+        load_strip<IT>(t, desc->cols[c].base[src], desc->cols[c].width,
+                       desc->cols[c].stride[src], tbase, ebase, cnt);
+        store_strip<IT>(desc->cols[c].base[BUF_OUT], desc->cols[c].width,
+                        desc->cols[c].stride[BUF_OUT], tbase, ebase, cnt,
+                        [&](int k) { return t[k]; });
+      }
+    return;  // (uniform over the grid: no barrier follows)
+  }
+  const int rbits = 64 - __clzll((long long)var);
+  const int bits = choose_bits(n, rbits);
+  const int shift = rbits - bits;
+  const uint32_t nb = 1u << bits, mask = nb - 1;
+  if (has_tile) {
+    for (uint32_t b = threadIdx.x; b < kMaxBins; b += kScatterThreads) Ls.level.hist[b] = 0;
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < IT; k++)
+      if (valid(k))
+        atomicAdd(&Ls.level.hist[(uint32_t)(xf((U)(v0[k] & kmask)) >> shift) & mask], 1u);
+    __syncthreads();
+    for (uint32_t b = threadIdx.x; b < nb; b += kScatterThreads)
+      hist[(size_t)w * kMaxBins + b] = Ls.level.hist[b];
+  }
+  grid.sync();
+
+  // ---- 3. offsets; the stable scatter of the tile into TMP
+  {
+    // the T x nb counts into LDS in one round of loads, then summed per bucket
+    const int TN = T * (int)nb;  // (<= kMidMat: the host sizes the launch)
+    uint32_t cv[kMidMat / kScatterThreads];
+#pragma unroll
+    for (int k = 0; k < kMidMat / kScatterThreads; k++) {
+      const int e = (int)threadIdx.x + k * kScatterThreads;
+      cv[k] = e < TN ? hist[(size_t)(e >> bits) * kMaxBins + (e & mask)] : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < kMidMat / kScatterThreads; k++) {
+      const int e = (int)threadIdx.x + k * kScatterThreads;
+      if (e < TN) Ls.level.mat[e] = cv[k];
+    }
+    __syncthreads();
+    const uint32_t b = threadIdx.x;  // (kScatterThreads >= kMaxBins: one bin per thread)
+    uint32_t tot = 0, pre = 0;
+    if (b < nb)
+      for (int i = 0; i < T; i++) {
+        const uint32_t c = Ls.level.mat[i * nb + b];
+        tot += c;
+        pre += i < w ? c : 0u;
+      }
+    uint32_t all;
+    const uint32_t bs = block_excl_scan<kScatterThreads, uint32_t>(tot, Ls.level.sc.scan_sh, &all);
+    if (b == (uint32_t)w) {  // (this workgroup's bucket, for phase 4)
+      my_start = b < nb ? (int64_t)bs : 0;
+      my_len = b < nb ? (int32_t)tot : 0;
+    }
+    // the host learns now how many buckets come back to it, not at the end
+    const int nbig = __syncthreads_count(b < nb && tot > (uint32_t)kLocalCap && shift > 0);
+    if (w == 0 && threadIdx.x == 0)
+      mid_tell_host(flag, (unsigned long long)nbig | (nb > (uint32_t)G || TN > kMidMat ? 1ull << 63 : 0), seq);
+    if (has_tile) {
+      if (threadIdx.x == 0) {
+        SegPlan& P = Ls.level.plan;
+        P.start = 0;
+        P.len = n;
+        P.tile_base = 0;
+        P.group_base = 0;
+        P.ntiles = T;
+        P.ngroups = 1;
+        P.shift = shift;
+        P.bits = bits;
+        P.buf = src;
+        P.dst = BUF_TMP;
+        P.skip = 0;
+      }
+      __syncthreads();
+      TileInfo ti;
+      ti.base = tbase;
+      ti.cnt = cnt;
+      ti.s = 0;
+      ti.t = w;
+      const int64_t my_off = b < nb ? (int64_t)bs + pre : 0;
+      scatter_process_tile<KT, U, 0, CZ, false>(desc, &Ls.level.plan, Ls.level.sc, ti, ncols, v0,
+                                                 v1, v2, my_off, DigitLut{});
+    }
+  }
+  grid.sync();
+
+  // ---- 4. bucket w, into OUT
+  const int32_t len = my_len;
+  if (len == 0) return;
+  const Seg g{my_start, (int64_t)len, shift, BUF_TMP};
+  if (len > kLocalCap && shift > 0) {  // (skewed keys: the host's general levels take it)
+    if (threadIdx.x == 0) big[atomicAdd(&ctr->n_big, 1ull)] = g;
+    return;
+  }
+  if (len > kLocalCap) {  // one key value (no bits below the digit): TMP holds it in order
+    for (int c = 0; c < ncols; c++) {
+      const Col& C = desc->cols[c];
+      with_width(C.width, [&](auto W_) {
+        constexpr int WB = decltype(W_)::value;
+        for (int64_t i = threadIdx.x; i < len; i += kLocalThreads) {
+          const int64_t r = my_start + i;
+          stw<WB>(C.base[BUF_OUT] + r * C.stride[BUF_OUT], ldw<WB>(C.base[BUF_TMP] + r * C.stride[BUF_TMP]));
+        }
+      });
+    }
+    return;
+  }
+  int path = 0;
+  if (local_fast_body<KT, U, kLocalThreads, kLocalItems, CZ>(desc, g, Ls.local.fast, [] {})) {
+    __syncthreads();
+    path = 1;
+    if (local_stable_body<KT, U, kLocalStableThreads, CZ>(desc, g, Ls.local.stable)) {
+      __syncthreads();
+      path = 2;
+      local_lsd_body<KT, U, CZ>(desc, g, Ls.local.lsd);
+    }
+  }
+  if (threadIdx.x == 0 && path) {
+    atomicMax(&taken[0], 1ull);
+    if (path >= 2) atomicMax(&taken[1], 1ull);
+  }
+}
+
+// ---------------------------------------------------------------------------
 // sampled 16-bit key histogram (balanced first level): chunk c
 // = keys [c*stride, c*stride + chunk). Each of kSampleWGs workgroups counts
 // its share of the chunks into LDS-private u16 bins (64K bins packed in
@@ -3770,6 +4042,25 @@ void launch_local_lsd(int key_size, const SortDesc* d, const Seg* segs,
   local_lsd_kernel<KT, U, CZ><<<(unsigned)grid, kLocalStableThreads, 0, st>>>(d, segs, nsegs)
   SRS_KEY_DISPATCH(key_size, CALL)
 #undef CALL
+}
+
+hipError_t launch_mid_sort(int key_size, const SortDesc& d, int64_t n, int src,
+                           unsigned long long* part, uint32_t* hist, ListCounters* ctr, Seg* big,
+                           unsigned long long* taken, MidFlag* flag, unsigned long long seq,
+                           hipStream_t st) {
+  const unsigned T = (unsigned)((n + kTile - 1) / kTile);
+  const unsigned nb_max = 1u << choose_bits(n, 64);
+  if (T > (unsigned)kMidMaxTiles || T * nb_max > (unsigned)kMidMat) return hipErrorInvalidValue;
+  const unsigned G = std::max(T, nb_max);  // (one bucket per workgroup)
+  SortDesc dd = d;
+  int32_t s32 = src;
+  void* args[] = {&dd, &n, &s32, &part, &hist, &ctr, &big, &taken, &flag, &seq};
+#define CALL(KT, U, CZ)                                                                         \
+  return hipLaunchCooperativeKernel((const void*)mid_sort_kernel<KT, U, CZ>, dim3(G),          \
+                                    dim3(kLocalThreads), args, 0, st)
+  SRS_KEY_DISPATCH(key_size, CALL)
+#undef CALL
+  return hipErrorInvalidValue;
 }
 
 void launch_small_sort(int key_size, const SortDesc& d, Seg g, int64_t* taken, hipStream_t st) {
