@@ -99,3 +99,21 @@ def test_c3_aos16_vs_reference(torch, up):
     ref_sort_aos(srs_amd.KEY_U64, up, r_ref)
     torch.cuda.synchronize()
     assert np.array_equal(out.cpu().numpy().view(np.uint8).reshape(N, 16), r_ref)
+
+
+def test_c0_u32_keys_only_vs_reference(torch):
+    """C0 (BASELINE configs[0]): 1e6 uint32 keys, no payload, ascending, through
+    the host-array entry point (radixSort.hpp:1780 with no payload), against
+    the reference's own sort and the oracle restatement."""
+    from srs_testlib import oracle_sort_soa
+    n = 10**6
+    rng = np.random.default_rng(2024)
+    keys = rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32)
+    k = keys.copy()
+    srs_amd.sort(k)
+    k_ref = keys.copy()
+    ref_sort_soa(srs_amd.KEY_U32, True, k_ref, [])
+    assert np.array_equal(k, k_ref), "keys differ from the reference"
+    k_or = keys.copy()
+    oracle_sort_soa(srs_amd.KEY_U32, True, k_or, [])
+    assert np.array_equal(k, k_or), "keys differ from the oracle"
