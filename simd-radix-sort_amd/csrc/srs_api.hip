@@ -1708,6 +1708,7 @@ int run_sort(Workspace* W, const Request& R, hipStream_t st) {
   SRS_TRY(ensure(W->totals, 4 * sizeof(uint64_t)));
   ListCounters* d_ctr = (ListCounters*)W->ctr.p;
   int64_t n_big = 0, n_local = 0, n_local2 = 0, n_copy = 0;
+  bool mid_continued = false;  // (the big list came from the mid-size launch)
   if (R.nsegs > 0) {
     // independent segments (multi-GPU receive groups): sorted as sub-ranges
     // of one sort, each starting at the full key width (the varying-bit
@@ -1748,52 +1749,66 @@ int run_sort(Workspace* W, const Request& R, hipStream_t st) {
     n_local = (int64_t)hl.size();
     n_local2 = (int64_t)hl2.size();
     W->h_ctr->local_elems = lel;
-  } else if (mid) {
-    // one cooperative launch: the first level and every bucket's local sort;
-    // buckets over kLocalCap (skewed keys) come back in the big list and
-    // continue on the general levels below
-    const int64_t G = (n + kTile - 1) / kTile;
-    SRS_TRY(ensure(W->mid, G * 16 + G * kMaxBins * sizeof(uint32_t)));
-    DevBuf& taken = W->small_taken[st];
-    SRS_TRY(ensure(taken, 2 * sizeof(int64_t)));
-    hipError_t e;
-    const unsigned long long seq = ++W->mid_seq;
-    {
-      note_elems("mid", (double)n);
-      TimedScope ts("mid", (double)0, st);
-      e = launch_mid_sort(ksl, d, n, home, (unsigned long long*)W->mid.p,
-                          (uint32_t*)((char*)W->mid.p + G * 16), d_ctr, (Seg*)W->big[0].p,
-                          (unsigned long long*)taken.p, W->h_mid, seq, st);
-    }
-    if (e != hipSuccess) return fail(SRS_ERR_HIP, std::string("mid-size launch: ") +
-                                                      hipGetErrorString(e));
-    // The kernel's workgroup 0 posts the big-bucket count to host memory once
-    // the first level's sizes are known (MidFlag): polled for a while (a
-    // stream sync's wake-up cost ~30 us per call), then waited for
-    SRS_TRY(wait_mid_flag(W->h_mid, seq, st));
-    const unsigned long long nb_flag = __atomic_load_n(&W->h_mid->n_big, __ATOMIC_ACQUIRE);
-    if (nb_flag >> 63) return fail(SRS_ERR_INTERNAL, "mid-size launch: more buckets than workgroups");
-    n_big = (int64_t)nb_flag;
-    if (n_big == 0) {
-      W->last_small = true;  // (srs_debug_last_fallbacks reads `taken`)
-      W->last_small_stream = st;
-      return SRS_OK;
-    }
-    launch_set_desc(d, d_desc, st);
-    W->h_ctr->local_elems = 0;
   } else {
-    Seg seg0{0, n, d.key_bits, home};
-    const bool to_local = n <= kLocalCap;
-    launch_start(d, d_desc, seg0, to_local ? 1 : 0, (Seg*)W->big[0].p, (Seg*)W->local.p,
-                 (Seg*)W->local2.p, d_ctr, st);
-    n_big = to_local ? 0 : 1;
-    n_local = (to_local && n <= kLocalCapSmall) ? 1 : 0;
-    n_local2 = (to_local && n > kLocalCapSmall) ? 1 : 0;
-    W->h_ctr->local_elems = to_local ? (uint64_t)n : 0;
+    bool started = false;  // (by the mid-size launch)
+    if (mid) {
+      // one cooperative launch: the first level and every bucket's local
+      // sort; buckets over kLocalCap (skewed keys) come back in the big list
+      // and continue on the general levels below
+      const int64_t T = (n + kTile - 1) / kTile;
+      SRS_TRY(ensure(W->mid, T * 16 + T * kMaxBins * sizeof(uint32_t)));
+      DevBuf& taken = W->small_taken[st];
+      SRS_TRY(ensure(taken, 2 * sizeof(int64_t)));
+      hipError_t e;
+      const unsigned long long seq = ++W->mid_seq;
+      {
+        note_elems("mid", (double)n);
+        TimedScope ts("mid", (double)0, st);
+        e = launch_mid_sort(ksl, d, n, home, (unsigned long long*)W->mid.p,
+                            (uint32_t*)((char*)W->mid.p + T * 16), d_ctr, (Seg*)W->big[0].p,
+                            (unsigned long long*)taken.p, W->h_mid, seq, st);
+      }
+      if (e != hipSuccess) {
+        // (a cooperative launch the device cannot take: the general path,
+        // which the column layout chosen for `mid` also serves)
+        (void)hipGetLastError();
+        if (trace_levels())
+          fprintf(stderr, "[srs] mid-size launch refused (%s): general path\n", hipGetErrorString(e));
+      } else {
+        // The kernel's workgroup 0 posts the big-bucket count to host memory
+        // once the first level's sizes are known (MidFlag): polled for a
+        // while (a stream sync's wake-up cost ~30 us per call), then waited for
+        SRS_TRY(wait_mid_flag(W->h_mid, seq, st));
+        const unsigned long long nb_flag = __atomic_load_n(&W->h_mid->n_big, __ATOMIC_ACQUIRE);
+        if (nb_flag >> 63)
+          return fail(SRS_ERR_INTERNAL, "mid-size launch: more buckets than workgroups");
+        n_big = (int64_t)nb_flag;
+        if (n_big == 0) {
+          W->last_small = true;  // (srs_debug_last_fallbacks reads `taken`)
+          W->last_small_stream = st;
+          return SRS_OK;
+        }
+        launch_set_desc(d, d_desc, st);
+        W->h_ctr->local_elems = 0;
+        started = true;
+      }
+    }
+    if (!started) {
+      Seg seg0{0, n, d.key_bits, home};
+      const bool to_local = n <= kLocalCap;
+      launch_start(d, d_desc, seg0, to_local ? 1 : 0, (Seg*)W->big[0].p, (Seg*)W->local.p,
+                   (Seg*)W->local2.p, d_ctr, st);
+      n_big = to_local ? 0 : 1;
+      n_local = (to_local && n <= kLocalCapSmall) ? 1 : 0;
+      n_local2 = (to_local && n > kLocalCapSmall) ? 1 : 0;
+      W->h_ctr->local_elems = to_local ? (uint64_t)n : 0;
+    } else {
+      mid_continued = true;
+    }
   }
   LevelState S{n_big, n_local, n_local2, n_copy, 0, d.ncols, d.tmp2};
   S.pair_tiles = pair_tiles_mode(d, ks);
-  if (R.nsegs == 0 && n_big == 1 && !mid) S.known_len = n;
+  if (R.nsegs == 0 && n_big == 1 && !mid_continued) S.known_len = n;
   int level = 0;
   // Stripe first level: large plain SoA sorts partition
   // stripes of kStripeKeysPerBucket << b1 keys on their own with the first

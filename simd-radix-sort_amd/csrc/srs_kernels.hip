@@ -345,12 +345,12 @@ __device__ __forceinline__ T block_excl_scan(T v, T* sh, T* total) {
 #define SRS_STAMPS 0
 #endif
 #if SRS_STAMPS
-#define STAMP_DECL unsigned long long ts_[8] = {0}; int tsn_ = 0;
+#define STAMP_DECL unsigned long long ts_[16] = {0}; int tsn_ = 0;
 #define STAMP()                                                              \
   do {                                                                       \
     if (threadIdx.x == 0) {                                                  \
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");            \
-      if (tsn_ < 8) ts_[tsn_++] = __builtin_amdgcn_s_memtime();              \
+      if (tsn_ < 16) ts_[tsn_++] = __builtin_amdgcn_s_memtime();              \
     }                                                                        \
   } while (0)
 #define STAMP_FLUSH(kid)                                                     \
@@ -622,14 +622,49 @@ __global__ void seg_map2_kernel(const int64_t* __restrict__ tbase, int64_t ntile
 // neighbouring tiles write into the same bucket meet in one L2. Bijective for
 // any grid size. Placement only affects speed, never results.
 // The OR of every thread's `v` into the workgroup's slots, one per wave:
-// each wave resets its own slot first (a wave's LDS operations take effect in
-// program order), so no block-wide reset has to be ordered before the other
-// waves' atomics. The caller barriers, then reads wave_or_read.
+// reduced across the wave first, then one plain store per wave (64 lanes'
+// LDS atomics on one address serialise: with them, this step took ~3 us of
+// a small sort's 12). The caller barriers, then reads wave_or_read.
+// (DPP row operations, no LDS crossbar and no address registers: the
+// quad_perms, half-row and row mirrors leave each row's OR in all its lanes,
+// row_bcast:15 / :31 carry rows 0-2 into row 3; lane 63 holds the result)
+__device__ __forceinline__ uint32_t wave_or32(uint32_t v) {
+  v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);   // quad [1,0,3,2]
+  v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);   // quad [2,3,0,1]
+  v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false);  // row_half_mirror
+  v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xF, 0xF, false);  // row_mirror
+  v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);  // row_bcast:15
+  v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);  // row_bcast:31
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+__device__ __forceinline__ unsigned long long wave_or(unsigned long long v) {
+  return ((unsigned long long)wave_or32((uint32_t)(v >> 32)) << 32) | wave_or32((uint32_t)v);
+}
+// max over the wave of v in [0, 2^15) from 15 ballots (scalar masks: no
+// vector registers beyond the compares)
+__device__ __forceinline__ int wave_max(int v) {
+  uint64_t cand = __ballot(true);
+  int r = 0;
+#pragma unroll
+  for (int b = 14; b >= 0; b--) {
+    const uint64_t m = __ballot((v >> b) & 1) & cand;
+    if (m) {
+      cand = m;
+      r |= 1 << b;
+    }
+  }
+  return r;
+}
+// atomicMax of every thread's m into one LDS word: one atomic per wave
+__device__ __forceinline__ void block_max_into(int* dst, int m) {  // (m < 2^15: bucket sizes)
+  m = wave_max(m);
+  if (lane_id() == 0 && m > 0) atomicMax(dst, m);
+}
 template <int NW>
 __device__ __forceinline__ void wave_or_add(unsigned long long (&wor)[NW], uint32_t wave,
                                             uint32_t lane, unsigned long long v) {
-  if (lane == 0) wor[wave] = 0;
-  if (v) atomicOr(&wor[wave], v);
+  v = wave_or(v);
+  if (lane == 0) wor[wave] = v;
 }
 template <int NW>
 __device__ __forceinline__ unsigned long long wave_or_read(const unsigned long long (&wor)[NW]) {
@@ -2082,8 +2117,11 @@ __device__ __forceinline__ bool local_fast_body(const SortDesc* __restrict__ des
     if (valid(k)) vor |= ukey(k) ^ uref;
   STAMP();  // 1: keys loaded
   wave_or_add(Ls.wor, wave, lane, (unsigned long long)vor);
+  STAMP();  // (diag) or reduced
   lds_barrier();
+  STAMP();  // (diag) barrier passed
   const unsigned long long var = wave_or_read(Ls.wor);
+  STAMP();  // (diag) var
 
   if (var != 0) {
     const int lo = __ffsll((long long)var) - 1;
@@ -2177,6 +2215,7 @@ __device__ __forceinline__ bool local_fast_body(const SortDesc* __restrict__ des
                         desc->cols[0].stride[BUF_IN] == (uint32_t)kbytes;
     auto bucket_rank = [&](auto DIRECT_) -> bool {
     constexpr bool DIRECT = decltype(DIRECT_)::value;
+    STAMP();  // (diag) direct decided
     // ---- 2. bucket pass on the top varying bits (LDS atomics on 16-bit
     // counters packed in pairs: 2^11 buckets in the LDS of 2^10 u32 ones) ----
 #pragma unroll
@@ -2186,7 +2225,9 @@ __device__ __forceinline__ bool local_fast_body(const SortDesc* __restrict__ des
         atomicAdd(&hist2[d >> 1], 1u << ((d & 1) << 4));
       }
     }
+    STAMP();  // (diag) atomics issued
     lds_barrier();
+    STAMP();  // (diag) barrier
     {
       uint32_t tb[BPT], tsum = 0;
 #pragma unroll
@@ -2198,6 +2239,7 @@ __device__ __forceinline__ bool local_fast_body(const SortDesc* __restrict__ des
       }
       uint32_t tot;
       uint32_t ex = block_excl_scan_1b<NT>(tsum, scan_sh, &tot);
+      STAMP();  // (diag) scanned
       int mymax = 0;
 #pragma unroll
       for (int q = 0; q < BPT; q += 2) {
@@ -2210,7 +2252,7 @@ __device__ __forceinline__ bool local_fast_body(const SortDesc* __restrict__ des
         mymax = max(mymax, (int)max(tb[q], tb[q + 1]));
       }
       if (threadIdx.x == 0) bin_start[NB] = (uint16_t)tot;
-      if (mymax > 0) atomicMax(&maxlen, mymax);
+      block_max_into(&maxlen, mymax);
     }
     lds_barrier();
     STAMP();  // 2: bucket histogram
@@ -2764,7 +2806,7 @@ __global__ __launch_bounds__(NT, WPE) void local_direct_kernel(
         ex = e1 + tb[q + 1];
         mymax = max(mymax, (int)max(tb[q], tb[q + 1]));
       }
-      if (mymax > 0) atomicMax(&Ls.maxlen, mymax);
+      block_max_into(&Ls.maxlen, mymax);
     }
     lds_barrier();
     const int maxlen = __builtin_amdgcn_readfirstlane(Ls.maxlen);
@@ -2980,7 +3022,10 @@ with_width(w, [&](auto W_) {
 #pragma unroll
   for (int k = 0; k < IT; k++)
     if (valid(k)) vor |= ukey(k) ^ uref;
-  if (vor) atomicOr(&sh_or, (unsigned long long)vor);
+  {
+    const unsigned long long wv = wave_or((unsigned long long)vor);  // (one atomic per wave)
+    if (lane == 0 && wv) atomicOr(&sh_or, wv);
+  }
   lds_barrier();
   const unsigned long long var = sh_or;
 
@@ -3072,7 +3117,7 @@ with_width(w, [&](auto W_) {
         const int len = (int)(bin_start[b + 1] - bin_start[b]);
         if (bflag[b] && len > mymax) mymax = len;
       }
-      if (mymax > 0) atomicMax(&maxlen, mymax);
+      block_max_into(&maxlen, mymax);
     }
     lds_barrier();
     if (maxlen > kRankSortMax) {
@@ -3206,21 +3251,22 @@ __global__ __launch_bounds__(NT) void local_stable_kernel(
 // Fallback for segments whose top-digit buckets are too large for the rank
 // step (skewed keys): stable LSD passes (ballot ranks) over every varying
 // bit. Grid-stride over a device-side list whose length is read on device.
+template <int NT>
 struct LsdLds {
-  static constexpr int CAP = kLocalStableThreads * kLocalStableItems;
+  static constexpr int CAP = NT * kLocalStableItems;
   uint64_t sbuf[CAP];
   uint16_t sidx[CAP];
-  uint16_t wc[kLocalStableThreads / 64][1 << kLocalBits];
+  uint16_t wc[NT / 64][1 << kLocalBits];
   uint32_t bin_start[(1 << kLocalBits) + 1];
-  uint32_t scan_sh[kLocalStableThreads / 64 + 1];
+  uint32_t scan_sh[NT / 64 + 1];
   unsigned long long sh_or;
 };
 
-// One segment g by one workgroup of kLocalStableThreads (always finishes it).
-template <typename KT, typename U, bool CZ>
+// One segment g (<= NT * kLocalStableItems records) by one workgroup of NT
+// threads (always finishes it).
+template <typename KT, typename U, bool CZ, int NT = kLocalStableThreads>
 __device__ __forceinline__ void local_lsd_body(const SortDesc* __restrict__ desc, const Seg g,
-                                               LsdLds& Ls) {
-  constexpr int NT = kLocalStableThreads;
+                                               LsdLds<NT>& Ls) {
   constexpr int IT = kLocalStableItems;
   auto& sbuf = Ls.sbuf;
   auto& sidx = Ls.sidx;
@@ -3266,7 +3312,10 @@ __device__ __forceinline__ void local_lsd_body(const SortDesc* __restrict__ desc
 #pragma unroll
     for (int k = 0; k < IT; k++)
       if (valid[k]) vor |= u[k] ^ uref;
-    if (vor) atomicOr(&sh_or, (unsigned long long)vor);
+    {
+      const unsigned long long wv = wave_or((unsigned long long)vor);  // (one atomic per wave)
+      if (lane_id() == 0 && wv) atomicOr(&sh_or, wv);
+    }
     __syncthreads();
     const unsigned long long var = sh_or;
     if (var != 0) {
@@ -3314,7 +3363,7 @@ template <typename KT, typename U, bool CZ>
 __global__ __launch_bounds__(kLocalStableThreads) void local_lsd_kernel(
     const SortDesc* __restrict__ desc, const Seg* __restrict__ segs,
     const unsigned long long* __restrict__ nsegs) {
-  __shared__ LsdLds Ls;
+  __shared__ LsdLds<kLocalStableThreads> Ls;
   const unsigned long long total = *nsegs;
   for (unsigned long long si = blockIdx.x; si < total; si += gridDim.x)
     local_lsd_body<KT, U, CZ>(desc, segs[si], Ls);
@@ -3331,31 +3380,53 @@ __global__ __launch_bounds__(kLocalStableThreads) void local_lsd_kernel(
 static_assert(kLocalStableThreads == kLocalThreads, "the three bodies share one workgroup");
 static_assert(sizeof(SortDesc) + sizeof(Seg) + sizeof(int64_t*) <= 4096,
               "small_sort_kernel's arguments fit the 4 KB kernel-argument segment");
-union SmallLds {
-  FastLds<kLocalThreads, kLocalItems> fast;
-  StableLds<kLocalStableThreads> stable;
-  LsdLds lsd;
+static_assert(kLocalItems == kLocalStableItems, "the three bodies hold the same records per thread");
+template <int NT>
+union SmallLdsT {
+  FastLds<NT, kLocalItems> fast;
+  StableLds<NT> stable;
+  LsdLds<NT> lsd;
 };
+using SmallLds = SmallLdsT<kLocalThreads>;
 
-template <typename KT, typename U, bool CZ>
-__global__ __launch_bounds__(kLocalThreads) void small_sort_kernel(const SortDesc d, const Seg g,
-                                                                   int64_t* taken) {
-  __shared__ SmallLds Ls;
-  const SortDesc* desc = &d;
+// NT threads for n <= NT * 8 records: a 1024-thread workgroup puts four
+// waves on each SIMD, and every wave issues every (predicated) instruction of
+// the bodies whether it holds records or not, so a small sort's time follows
+// the waves, not the records (1024 keys: 11 us with 16 waves)
+// The three bodies in turn over one segment; returns 0 (fast), 1 (stable)
+// or 2 (LSD): the last body that ran.
+template <typename KT, typename U, bool CZ, int NT>
+__device__ __forceinline__ int small_bodies(const SortDesc* __restrict__ desc, const Seg g,
+                                            SmallLdsT<NT>& Ls) {
   int path = 0;
-  if (local_fast_body<KT, U, kLocalThreads, kLocalItems, CZ>(desc, g, Ls.fast, [] {})) {
+  if (local_fast_body<KT, U, NT, kLocalItems, CZ>(desc, g, Ls.fast, [] {})) {
     __syncthreads();  // the fast body's LDS is reused
     path = 1;
-    if (local_stable_body<KT, U, kLocalStableThreads, CZ>(desc, g, Ls.stable)) {
+    if (local_stable_body<KT, U, NT, CZ>(desc, g, Ls.stable)) {
       __syncthreads();
       path = 2;
-      local_lsd_body<KT, U, CZ>(desc, g, Ls.lsd);
+      local_lsd_body<KT, U, CZ, NT>(desc, g, Ls.lsd);
     }
   }
+  return path;
+}
+
+template <typename KT, typename U, bool CZ, int NT>
+__global__ __launch_bounds__(NT) void small_sort_kernel(const SortDesc d, const Seg g,
+                                                        int64_t* taken) {
+  __shared__ SmallLdsT<NT> Ls;
+  const SortDesc* desc = &d;
+  const int path = small_bodies<KT, U, CZ, NT>(desc, g, Ls);
   if (threadIdx.x == 0 && taken) {
     taken[0] = path >= 1;
     taken[1] = path >= 2;
   }
+#ifdef SRS_DIAG_TWICE
+  // diagnostic (timing only): the sort again over its own output, so that a
+  // kernel trace shows what a second, warm pass through the same code costs
+  __syncthreads();
+  small_bodies<KT, U, CZ, NT>(desc, Seg{g.start, g.len, g.rbits, BUF_OUT}, Ls);
+#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -3613,15 +3684,16 @@ __global__ __launch_bounds__(kLocalThreads) void mid_sort_kernel(
     }
     return;
   }
-  int path = 0;
-  if (local_fast_body<KT, U, kLocalThreads, kLocalItems, CZ>(desc, g, Ls.local.fast, [] {})) {
-    __syncthreads();
-    path = 1;
-    if (local_stable_body<KT, U, kLocalStableThreads, CZ>(desc, g, Ls.local.stable)) {
-      __syncthreads();
-      path = 2;
-      local_lsd_body<KT, U, CZ>(desc, g, Ls.local.lsd);
-    }
+  // (a bucket of <= 4096 records by the first 512 threads: waves 8-15 end
+  // here, and the bodies' barriers wait for the surviving waves only; eight
+  // waves instead of sixteen issue the bodies' instructions, as in the small
+  // sort's shapes)
+  int path;
+  if (len <= 512 * kLocalItems) {
+    if (threadIdx.x >= 512) return;
+    path = small_bodies<KT, U, CZ, 512>(desc, g, *reinterpret_cast<SmallLdsT<512>*>(&Ls.local));
+  } else {
+    path = small_bodies<KT, U, CZ, kLocalThreads>(desc, g, Ls.local);
   }
   if (threadIdx.x == 0 && path) {
     atomicMax(&taken[0], 1ull);
@@ -4064,8 +4136,19 @@ hipError_t launch_mid_sort(int key_size, const SortDesc& d, int64_t n, int src,
 }
 
 void launch_small_sort(int key_size, const SortDesc& d, Seg g, int64_t* taken, hipStream_t st) {
-#define CALL(KT, U, CZ) \
-  small_sort_kernel<KT, U, CZ><<<1, kLocalThreads, 0, st>>>(d, g, taken)
+  static_assert(kLocalThreads == 1024, "the small sort's shapes");
+  const int64_t n = g.len;
+#define CALL(KT, U, CZ)                                                       \
+  do {                                                                        \
+    if (n <= 128 * kLocalItems)                                               \
+      small_sort_kernel<KT, U, CZ, 128><<<1, 128, 0, st>>>(d, g, taken);      \
+    else if (n <= 256 * kLocalItems)                                          \
+      small_sort_kernel<KT, U, CZ, 256><<<1, 256, 0, st>>>(d, g, taken);      \
+    else if (n <= 512 * kLocalItems)                                          \
+      small_sort_kernel<KT, U, CZ, 512><<<1, 512, 0, st>>>(d, g, taken);      \
+    else                                                                      \
+      small_sort_kernel<KT, U, CZ, 1024><<<1, 1024, 0, st>>>(d, g, taken);    \
+  } while (0)
   SRS_KEY_DISPATCH(key_size, CALL)
 #undef CALL
 }
