@@ -2039,7 +2039,12 @@ __device__ __forceinline__ void local_digit_pass(
 // Fast path: bucket pass with LDS atomics (order inside a bucket arbitrary);
 // the rank step then restores the stable order from the packed
 // (key bits, original index) words.
-template <int NT, int IT>
+// TB: the atomic bucket pass's digit bits (the exact pass keeps
+// kLocalTopBits). The small sorts take one or two more: a whole small sort of
+// full-range 64-bit keys then packs (the 52 / 51 key bits below a 12 / 13-bit
+// digit, index) into a word, where 11 bits left it to the stable kernel at
+// twice the time
+template <int NT, int IT, int TB = kLocalTopBits>
 struct FastLds {
   // sbuf: packed sort words (+ rank sentinels) during the sort, column
   // staging afterwards
@@ -2047,10 +2052,10 @@ struct FastLds {
   // __shared__ arrays)
   uint64_t sbuf[NT * IT + kRankSortMax];
   uint16_t perm[NT * IT];                      // output slot -> original index
-  uint16_t bin_start[(1 << kLocalTopBits) + 2];
+  uint16_t bin_start[(1 << TB) + 2];
   int maxlen;
   unsigned long long wor[NT / 64];             // varying-bit OR, one slot per wave (wave_or)
-  uint32_t hist2[(1 << kLocalTopBits) / 2];    // 16-bit bucket sizes, then cursors (pairs)
+  uint32_t hist2[(1 << TB) / 2];               // 16-bit bucket sizes, then cursors (pairs)
   uint32_t scan_sh[NT / 64 + 1];
 };
 
@@ -2059,14 +2064,16 @@ struct FastLds {
 // then); block-uniform.
 // bail() runs (every thread) right where the segment is handed over: the
 // grid kernel appends it to its fallback list there.
-template <typename KT, typename U, int NT, int IT, bool CZ, bool REC16 = false, typename Bail>
+template <typename KT, typename U, int NT, int IT, bool CZ, bool REC16 = false, typename Bail,
+          int TB>
 __device__ __forceinline__ bool local_fast_body(const SortDesc* __restrict__ desc, const Seg g,
-                                                FastLds<NT, IT>& Ls, Bail bail) {
+                                                FastLds<NT, IT, TB>& Ls, Bail bail) {
   constexpr int NW = NT / 64;
   constexpr int CAP = NT * IT;
   constexpr int IDXB = CAP <= 4096 ? 12 : 13;  // bits of an index inside the segment
   static_assert((1 << IDXB) >= CAP, "index bits");
-  constexpr int NB = 1 << kLocalTopBits;
+  static_assert(TB >= kLocalTopBits, "the exact pass's counters live in the bucket arrays' shape");
+  constexpr int NB = 1 << TB;
   constexpr int BPT = NB / NT;  // bins per thread (an even count: packed pairs)
   static_assert(BPT * NT == NB && BPT % 2 == 0, "bins per thread");
   static_assert(CAP < 65536, "16-bit bucket counters");
@@ -2127,7 +2134,7 @@ __device__ __forceinline__ bool local_fast_body(const SortDesc* __restrict__ des
     const int lo = __ffsll((long long)var) - 1;
     const int hi = 63 - __clzll((long long)var);
     const bool exact = hi - lo + 1 <= kLocalTopBits;
-    const int nbits = (hi - lo + 1) < kLocalTopBits ? (hi - lo + 1) : kLocalTopBits;
+    const int nbits = (hi - lo + 1) < TB ? (hi - lo + 1) : TB;
     const int sh = hi - nbits + 1;
     // The sort word packs (key bits 0..hi, original index) when that fits
     // in 64 bits. Wide segments (hi+1+IDXB > 64: mid-size sorts of 64-bit
@@ -2150,7 +2157,8 @@ __device__ __forceinline__ bool local_fast_body(const SortDesc* __restrict__ des
       // key value and a STABLE bucket pass (ballot ranks, input order inside
       // a bucket) is the final order. Duplicate-heavy data (C2's floats) lands
       // here; no bucket-size limit. Per-wave counters [NW][nb] live in sbuf.
-      constexpr bool kWcFits = NW * NB * sizeof(uint16_t) <= CAP * sizeof(uint64_t);
+      constexpr bool kWcFits =
+          NW * (1 << kLocalTopBits) * sizeof(uint16_t) <= CAP * sizeof(uint64_t);
       if constexpr (!kWcFits) {  // (tuning shapes only) the stable kernel takes it
         bail();
         return true;
@@ -3383,7 +3391,7 @@ static_assert(sizeof(SortDesc) + sizeof(Seg) + sizeof(int64_t*) <= 4096,
 static_assert(kLocalItems == kLocalStableItems, "the three bodies hold the same records per thread");
 template <int NT>
 union SmallLdsT {
-  FastLds<NT, kLocalItems> fast;
+  FastLds<NT, kLocalItems, (NT <= 512 ? 12 : 13)> fast;  // (see FastLds: TB)
   StableLds<NT> stable;
   LsdLds<NT> lsd;
 };

@@ -196,10 +196,20 @@ def test_sizes_u64_vs_oracle(n):
 
 def _fallback_keys(case, n, rng):
     if case in ("random64", "mid64"):
-        # random64 (one local segment): the full 64-bit range is too wide even for the fast
-        # kernel's below-digit words -> stable kernel (key-only words). mid64: after one
-        # global level the segments' ranges fit the fast kernel's wide mode -> no fallback
+        # random64 (one small sort): the full 64-bit range fits the small sort's
+        # below-digit words (12 / 13-bit bucket digit) -> no fallback. mid64:
+        # after one global level the segments' ranges fit the fast kernel's
+        # wide mode -> no fallback
         return rng.integers(0, 1 << 64, n, dtype=np.uint64)
+    if case == "wide_dups":
+        # wide keys and 200 copies of one value: the fast kernel hands
+        # the segment over (a bucket > 64 records), the stable kernel ranks
+        # key-only words (too wide for (key, index)) and keeps the equal
+        # bucket as it is
+        # (the copies alone in their top-10-bit bucket: the others < 2^63)
+        k = rng.integers(0, 1 << 63, n, dtype=np.uint64)
+        k[rng.choice(n, 200, replace=False)] = np.uint64(0xFFE0_1234_5678_9ABC)
+        return k
     if case == "dups":      # big all-equal buckets: fast kernel -> stable kernel
         k = np.full(n, 0x1234_5678_9ABC, dtype=np.uint64)
         m = rng.random(n) < 0.1
@@ -216,6 +226,7 @@ def _fallback_keys(case, n, rng):
 
 
 @pytest.mark.parametrize("case,n", [("random64", 16), ("random64", 3000), ("random64", 8000),
+                                    ("wide_dups", 3000), ("wide_dups", 8000),
                                     ("mid64", 1 << 20), ("mid64", 100_003),
                                     ("dups", 3000), ("dups", 8000), ("wide", 3000),
                                     ("wide", 8000), ("groups", 300_000)])
@@ -231,7 +242,7 @@ def test_local_fallback_paths(case, n):
     stable_n, lsd_n = srs_amd.last_fallbacks()
     order = np.argsort(keys, kind="stable")
     assert bytes_equal(k, keys[order]) and bytes_equal(p, idx[order])
-    if case == "mid64":
+    if case in ("mid64", "random64"):
         assert stable_n == 0 and lsd_n == 0, "the fast kernel should have sorted every segment"
         return
     assert stable_n > 0, "stable fallback not exercised"
