@@ -147,6 +147,7 @@ class Methods:
                 once()
             return sum(once() for _ in range(timed)) / timed / n
         # device-resident: input restored from a pristine copy between runs
+        self.last_gpu = []  # (per-call event times in us, for the progress line)
         src = torch.from_numpy(k.view(np.uint8)).cuda()
         dk = torch.empty_like(src)
         psrc = None if p is None else torch.from_numpy(p.view(np.uint8)).cuda()
@@ -168,6 +169,7 @@ class Methods:
             b.synchronize()
             if r >= warm:
                 tot += a.elapsed_time(b) * 1e6
+                self.last_gpu.append(a.elapsed_time(b) * 1e3)
         if not name.endswith("NoCmp"):
             out = dk.view(kt[ks]).cpu().numpy().view(k.dtype)
             if np.any(out[1:] < out[:-1]):
@@ -222,13 +224,28 @@ def main():
             continue
         for dist in args.dists.split(","):
             desc = tname + (f"-{args.payload}" if args.payload else "") + f"-{dist}"
-            rows = []
+            # one pass over the sizes per method (the same inputs in every
+            # pass): with the host-array calls interleaved between sizes, the
+            # device calls of 16K-128K keys measured ~45 us slower per call
+            # (kernels unchanged), which no isolated sequence
+            # reproduced
+            inputs = []
             for lg in range(0, args.max_log2 + 1):
                 n = 1 << lg
                 k = make(dtype, dist, n, rng)
                 p = None if pdt is None else make(pdt, "Uniform", n, rng)
-                rows.append((n, [m.measure(name, k, p) for name in m.names]))
-                print(desc, n, " ".join(f"{v:.3f}" for v in rows[-1][1]), flush=True)
+                inputs.append((n, k, p))
+            cols = {}
+            for name in m.names:
+                cols[name] = []
+                for n, k, p in inputs:
+                    cols[name].append(m.measure(name, k, p))
+                    extra = ""
+                    if name.startswith("GPURadix") and name != "GPURadixHost":
+                        g = sorted(getattr(m, "last_gpu", []) or [0.0])
+                        extra = f" (device calls: median {g[len(g) // 2]:.1f} us, max {g[-1]:.1f} us)"
+                    print(desc, name, n, f"{cols[name][-1]:.3f}" + extra, flush=True)
+            rows = [(n, [cols[name][i] for name in m.names]) for i, (n, _, _) in enumerate(inputs)]
             with open(os.path.join(args.out, f"tpe-{desc}.dat"), "w") as f:
                 f.write("number_of_elements " + " ".join(m.names) + "\n")
                 for n, vals in rows:
