@@ -474,6 +474,24 @@ int ensure_keep(DevBuf& b, size_t bytes, size_t live_bytes, hipStream_t st) {
   return SRS_OK;
 }
 
+// A short host wait on the sort's stream (a control read-back): polled for
+// up to 20 ms, then waited for. hipStreamSynchronize's blocking wake-up
+// costs ~30 us per call (the mid-size measurements), several
+// times per sort; a level's kernels take a few ms at most, so the poll ends
+// the wait in ~1 us.
+int sync_poll(hipStream_t st) {
+  const auto t0 = std::chrono::steady_clock::now();
+  for (;;) {
+    const hipError_t q = hipStreamQuery(st);
+    if (q == hipSuccess) return SRS_OK;
+    if (q != hipErrorNotReady) HIP_TRY(q);
+    if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(20)) break;
+    __builtin_ia32_pause();
+  }
+  HIP_TRY(hipStreamSynchronize(st));
+  return SRS_OK;
+}
+
 struct Workspace {
   DevBuf tmp;         // TMP data buffer (same footprint as the input)
   DevBuf tmp2;        // TMP2: AoS records as SoA slice columns (SortDesc::tmp2)
@@ -1083,7 +1101,7 @@ int plan_balanced_level(Workspace* W, const Request& R, const SortDesc& d, bool*
     return fail(SRS_ERR_INTERNAL, "sample histogram: too many keys per workgroup");
   std::vector<uint32_t> h(65536);
   HIP_TRY(hipMemcpyAsync(h.data(), W->shist.p, h.size() * 4, hipMemcpyDeviceToHost, st));
-  HIP_TRY(hipStreamSynchronize(st));
+  SRS_TRY(sync_poll(st));
   uint64_t total = 0, top9max = 0;
   for (int b = 0; b < 512; b++) {
     uint64_t t = 0;
@@ -1263,7 +1281,7 @@ int run_level(Workspace* W, int ks, const SortDesc* d_desc, LevelState& S, int f
   } else {
     HIP_TRY(hipMemcpyAsync(W->h_totals, d_totals, 4 * sizeof(uint64_t),
                            hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipStreamSynchronize(st));
+    SRS_TRY(sync_poll(st));
     ntiles = (int64_t)W->h_totals[0];
     ngroups = (int64_t)W->h_totals[1];
     level_keys = W->h_totals[3];
@@ -1338,7 +1356,7 @@ int run_level(Workspace* W, int ks, const SortDesc* d_desc, LevelState& S, int f
                          lut_rbits, st, (int32_t*)W->gorder.p, W->gorder_cap);
   }
   HIP_TRY(hipMemcpyAsync(W->h_ctr, d_ctr, sizeof(ListCounters), hipMemcpyDeviceToHost, st));
-  HIP_TRY(hipStreamSynchronize(st));
+  SRS_TRY(sync_poll(st));
   S.nbig = (int64_t)W->h_ctr->n_big;
   S.n_local = (int64_t)W->h_ctr->n_local;
   S.n_local2 = (int64_t)W->h_ctr->n_local2;
@@ -1530,7 +1548,7 @@ int plan_range_level(Workspace* W, const Request& R, const std::vector<KeyCluste
   HIP_TRY(hipMemcpyAsync(mm, init, sizeof init, hipMemcpyHostToDevice, st));
   launch_key_minmax(R.in_cols[0], ks, ks, R.num, d.mpos, d.mneg, hi, mm, st);
   HIP_TRY(hipMemcpyAsync(got.data(), mm, sizeof init, hipMemcpyDeviceToHost, st));
-  HIP_TRY(hipStreamSynchronize(st));
+  SRS_TRY(sync_poll(st));
   // the non-empty ranges (a range's keys: u in (hi[c-1], hi[c]])
   struct Rg {
     uint64_t mn, mx, cnt, hi;
