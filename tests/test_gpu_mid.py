@@ -167,3 +167,63 @@ def test_mid_fallback_counters():
     assert bytes_equal(k, keys[order]) and bytes_equal(p, idx[order])
     stable_n, lsd_n = srs_amd.last_fallbacks()
     assert stable_n >= 0 and lsd_n >= 0
+
+
+def test_mid_two_streams_and_threads():
+    """Mid-size sorts queued on two non-blocking streams, interleaved with a
+    small and a general-path sort, and from two host threads at once: the
+    launches share the workspace (its TMP, counters and the host-memory
+    flag), so each call must wait for the previous one's kernels and read
+    its own flag only. Every result against a stable sort."""
+    import threading
+    torch = _torch()
+    dev = torch.device("cuda:0")
+    streams = [torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev)]
+    sizes = [100_000, 5_000, 200_003, 3_000_000]
+    ins, outs = [], []
+    for i, n in enumerate(sizes):
+        k = torch.empty(n, dtype=torch.int64, device=dev)
+        p = torch.empty(n, dtype=torch.int64, device=dev)
+        srs_amd.fill_synthetic_device(k, p, seed=77 + i, key_kind=srs_amd.KEY_U64)
+        ins.append((k, p))
+        outs.append((torch.empty_like(k), torch.empty_like(p)))
+    torch.cuda.synchronize()
+    for _ in range(3):
+        for j, ((k, p), (ko, po)) in enumerate(zip(ins, outs)):
+            s = streams[j % 2]
+            s.wait_stream(torch.cuda.current_stream(dev))
+            srs_amd.sort_device(k, p, key_kind=srs_amd.KEY_U64, out=(ko, po), stream=s)
+    torch.cuda.synchronize()
+    for (k, p), (ko, po) in zip(ins, outs):
+        st = stable_reference(6, True, [k.cpu().numpy().view(np.uint64), p.cpu().numpy()])
+        assert bytes_equal(ko.cpu().numpy(), st[0]) and bytes_equal(po.cpu().numpy(), st[1])
+
+    errors = []
+
+    def worker(t):
+        try:
+            s = torch.cuda.Stream(device=dev)
+            rng = np.random.default_rng(t)
+            for it in range(10):
+                n = int(rng.integers(8193, 262145))
+                keys = rng.integers(0, 1 << 64, n, dtype=np.uint64)
+                idx = np.arange(n, dtype=np.uint64)
+                with torch.cuda.stream(s):
+                    dk = torch.from_numpy(keys.view(np.int64)).to(dev, non_blocking=False)
+                    dp = torch.from_numpy(idx.view(np.int64)).to(dev, non_blocking=False)
+                    s.synchronize()
+                    srs_amd.sort_device(dk, dp, key_kind=srs_amd.KEY_U64, stream=s)
+                    s.synchronize()
+                order = np.argsort(keys, kind="stable")
+                if not (bytes_equal(dk.cpu().numpy(), keys[order]) and
+                        bytes_equal(dp.cpu().numpy(), idx[order])):
+                    errors.append((t, it, n))
+        except Exception as e:  # (reported below)
+            errors.append((t, repr(e)))
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(2)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert not errors, errors
