@@ -1434,6 +1434,23 @@ bool is_inplace(const Request& R) {
   return inplace;
 }
 
+// The stream's slot for the single-launch sorts' fallback flags
+// (srs_debug_last_fallbacks). A caller that sorts on ever new streams would
+// grow the map without bound: past 64 streams the slots are dropped after a
+// device-wide wait (their kernels may still be writing them).
+int taken_slot(Workspace* W, hipStream_t st, DevBuf** out) {
+  if (W->small_taken.size() >= 64 && !W->small_taken.count(st)) {
+    HIP_TRY(hipDeviceSynchronize());
+    for (auto& t : W->small_taken) free_buf(t.second);
+    W->small_taken.clear();
+    W->last_small = false;
+  }
+  DevBuf& taken = W->small_taken[st];
+  SRS_TRY(ensure(taken, 2 * sizeof(int64_t)));
+  *out = &taken;
+  return SRS_OK;
+}
+
 // n <= kLocalCap (and no segment list): the whole sort is one local segment,
 // sorted by one single-workgroup launch that takes the descriptor as a kernel
 // argument. No workspace memory is touched (the input and output arrays
@@ -1452,8 +1469,9 @@ int run_small(Workspace* W, const Request& R, hipStream_t st) {
   set_columns(R, d, nullptr, nullptr, false, 0, nullptr, inplace);
   d.stamp_acc = g_stamp_acc;
   const Seg g{0, n, d.key_bits, inplace ? BUF_OUT : BUF_IN};
-  DevBuf& taken = W->small_taken[st];
-  SRS_TRY(ensure(taken, 2 * sizeof(int64_t)));
+  DevBuf* tk = nullptr;
+  SRS_TRY(taken_slot(W, st, &tk));
+  DevBuf& taken = *tk;
   W->last_small = true;
   W->last_small_stream = st;
   note_elems("local", (double)n);
@@ -1775,8 +1793,9 @@ int run_sort(Workspace* W, const Request& R, hipStream_t st) {
       // and continue on the general levels below
       const int64_t T = (n + kTile - 1) / kTile;
       SRS_TRY(ensure(W->mid, T * 16 + T * kMaxBins * sizeof(uint32_t)));
-      DevBuf& taken = W->small_taken[st];
-      SRS_TRY(ensure(taken, 2 * sizeof(int64_t)));
+      DevBuf* tk = nullptr;
+      SRS_TRY(taken_slot(W, st, &tk));
+      DevBuf& taken = *tk;
       hipError_t e;
       const unsigned long long seq = ++W->mid_seq;
       {

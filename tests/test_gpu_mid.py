@@ -227,3 +227,27 @@ def test_mid_two_streams_and_threads():
     for x in th:
         x.join()
     assert not errors, errors
+
+
+def test_many_streams_bound_the_flag_slots():
+    """Single-launch sorts on 70 fresh streams (small and mid-size): the
+    per-stream fallback-flag slots are recycled past 64 streams; every result
+    stays correct and srs_debug_last_fallbacks keeps answering."""
+    torch = _torch()
+    dev = torch.device("cuda:0")
+    rng = np.random.default_rng(70)
+    for i in range(70):
+        n = 5000 if i % 2 else 20000
+        keys = rng.integers(0, 1 << 64, n, dtype=np.uint64)
+        idx = np.arange(n, dtype=np.uint64)
+        s = torch.cuda.Stream(device=dev)
+        dk = torch.from_numpy(keys.view(np.int64)).to(dev)
+        dp = torch.from_numpy(idx.view(np.int64)).to(dev)
+        torch.cuda.synchronize()
+        srs_amd.sort_device(dk, dp, key_kind=srs_amd.KEY_U64, stream=s)
+        s.synchronize()
+        order = np.argsort(keys, kind="stable")
+        assert bytes_equal(dk.cpu().numpy(), keys[order]), i
+        assert bytes_equal(dp.cpu().numpy(), idx[order]), i
+        stable_n, lsd_n = srs_amd.last_fallbacks()
+        assert stable_n >= 0 and lsd_n >= 0
