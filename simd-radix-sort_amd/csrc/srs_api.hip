@@ -2126,6 +2126,7 @@ constexpr int kStageThreads = 4;
 constexpr int kStageBufs = 3;
 constexpr size_t kStageChunk = size_t(32) << 20;
 constexpr size_t kStageMinBytesDefault = size_t(16) << 20;  // below: one pageable hipMemcpy
+constexpr size_t kPackedMaxBytes = size_t(256) << 10;       // below: all columns in one DMA
 size_t stage_min_bytes() {  // (SRS_STAGE_MIN_MB overrides, for experiments)
   static const size_t v = [] {
     const char* e = getenv("SRS_STAGE_MIN_MB");
@@ -2300,11 +2301,26 @@ int host_sort_single(Request& R, int dev) {
   HIP_TRY(hipStreamSynchronize(st));  // (the previous call's kernels may still read stage)
   SRS_TRY(ensure(W->stage, total));
   Request D = R;
-  for (int c = 0; c < R.ncols; c++) {
-    char* dp = (char*)W->stage.p + off[c];
-    SRS_TRY(staged_copy(S, dp, (char*)R.in_cols[c], (size_t)R.num * col_width(R, c), true));
-    D.in_cols[c] = D.out_cols[c] = dp;
+  for (int c = 0; c < R.ncols; c++) D.in_cols[c] = D.out_cols[c] = (char*)W->stage.p + off[c];
+  if (total <= kPackedMaxBytes) {
+    // small: every column packed into one pinned buffer, one DMA each way (a
+    // pageable hipMemcpy per column and direction cost ~10-15 us each: 80 us
+    // per call of <= 8192 records of a key and a payload). Larger copies keep
+    // the pageable / staged paths, which overlap the host copy with the DMA.
+    char* pin = S->pin[0][0];
+    for (int c = 0; c < R.ncols; c++)
+      memcpy(pin + off[c], R.in_cols[c], (size_t)R.num * col_width(R, c));
+    HIP_TRY(hipMemcpyAsync(W->stage.p, pin, total, hipMemcpyHostToDevice, st));
+    SRS_TRY(run_sort(W, D, st));
+    HIP_TRY(hipMemcpyAsync(pin, W->stage.p, total, hipMemcpyDeviceToHost, st));
+    SRS_TRY(sync_poll(st));
+    for (int c = 0; c < R.ncols; c++)
+      memcpy(R.out_cols[c], pin + off[c], (size_t)R.num * col_width(R, c));
+    return SRS_OK;
   }
+  for (int c = 0; c < R.ncols; c++)
+    SRS_TRY(staged_copy(S, (char*)D.in_cols[c], (char*)R.in_cols[c],
+                        (size_t)R.num * col_width(R, c), true));
   SRS_TRY(run_sort(W, D, st));
   HIP_TRY(hipStreamSynchronize(st));
   for (int c = 0; c < R.ncols; c++)
