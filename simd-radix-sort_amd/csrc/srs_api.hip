@@ -2142,6 +2142,7 @@ struct HostStage {  // per device, kept between calls
   hipStream_t cst[kStageThreads] = {};  // copy streams (one per host thread)
   hipEvent_t ev[kStageThreads][kStageBufs] = {};
   hipStream_t st = nullptr;             // the sort's stream
+  char* zc = nullptr;                   // kPackedMaxBytes of coherent host memory (small sorts)
   // freed when the last holder lets go (as Workspace)
   ~HostStage() {
     for (int t = 0; t < kStageThreads; t++) {
@@ -2156,6 +2157,7 @@ struct HostStage {  // per device, kept between calls
       (void)hipStreamSynchronize(st);
       (void)hipStreamDestroy(st);
     }
+    if (zc) (void)hipHostFree(zc);
     (void)hipGetLastError();  // (nothing above may leave a sticky error behind)
   }
 };
@@ -2183,6 +2185,7 @@ int get_stage(int dev, StageRef* out) {
     }
   }
   HIP_TRY(hipStreamCreateWithFlags(&S->st, hipStreamNonBlocking));
+  HIP_TRY(hipHostMalloc((void**)&S->zc, kPackedMaxBytes, hipHostMallocCoherent));
   g_stage[dev] = S;
   *out = S;
   return SRS_OK;
@@ -2299,8 +2302,22 @@ int host_sort_single(Request& R, int dev) {
   WsUse use;
   SRS_TRY(use.begin(W, st));
   HIP_TRY(hipStreamSynchronize(st));  // (the previous call's kernels may still read stage)
-  SRS_TRY(ensure(W->stage, total));
   Request D = R;
+  if (total <= kPackedMaxBytes && R.nsegs == 0 && R.num <= kLocalCap) {
+    // a single-launch sort reads and writes the columns in coherent host
+    // memory itself (no DMA commands: a small kernel's PCIe round trips cost
+    // less than two copy launches and their waits)
+    for (int c = 0; c < R.ncols; c++) {
+      memcpy(S->zc + off[c], R.in_cols[c], (size_t)R.num * col_width(R, c));
+      D.in_cols[c] = D.out_cols[c] = S->zc + off[c];
+    }
+    SRS_TRY(run_sort(W, D, st));
+    SRS_TRY(sync_poll(st));
+    for (int c = 0; c < R.ncols; c++)
+      memcpy(R.out_cols[c], S->zc + off[c], (size_t)R.num * col_width(R, c));
+    return SRS_OK;
+  }
+  SRS_TRY(ensure(W->stage, total));
   for (int c = 0; c < R.ncols; c++) D.in_cols[c] = D.out_cols[c] = (char*)W->stage.p + off[c];
   if (total <= kPackedMaxBytes) {
     // small: every column packed into one pinned buffer, one DMA each way (a
