@@ -2127,6 +2127,7 @@ constexpr int kStageBufs = 3;
 constexpr size_t kStageChunk = size_t(32) << 20;
 constexpr size_t kStageMinBytesDefault = size_t(16) << 20;  // below: one pageable hipMemcpy
 constexpr size_t kPackedMaxBytes = size_t(256) << 10;       // below: all columns in one DMA
+constexpr size_t kZeroCopyMaxBytes = size_t(2) << 20;       // below: kernels on host memory
 size_t stage_min_bytes() {  // (SRS_STAGE_MIN_MB overrides, for experiments)
   static const size_t v = [] {
     const char* e = getenv("SRS_STAGE_MIN_MB");
@@ -2142,7 +2143,7 @@ struct HostStage {  // per device, kept between calls
   hipStream_t cst[kStageThreads] = {};  // copy streams (one per host thread)
   hipEvent_t ev[kStageThreads][kStageBufs] = {};
   hipStream_t st = nullptr;             // the sort's stream
-  char* zc = nullptr;                   // kPackedMaxBytes of coherent host memory (small sorts)
+  char* zc = nullptr;                   // kZeroCopyMaxBytes of coherent host memory
   // freed when the last holder lets go (as Workspace)
   ~HostStage() {
     for (int t = 0; t < kStageThreads; t++) {
@@ -2185,7 +2186,7 @@ int get_stage(int dev, StageRef* out) {
     }
   }
   HIP_TRY(hipStreamCreateWithFlags(&S->st, hipStreamNonBlocking));
-  HIP_TRY(hipHostMalloc((void**)&S->zc, kPackedMaxBytes, hipHostMallocCoherent));
+  HIP_TRY(hipHostMalloc((void**)&S->zc, kZeroCopyMaxBytes, hipHostMallocCoherent));
   g_stage[dev] = S;
   *out = S;
   return SRS_OK;
@@ -2303,10 +2304,10 @@ int host_sort_single(Request& R, int dev) {
   SRS_TRY(use.begin(W, st));
   HIP_TRY(hipStreamSynchronize(st));  // (the previous call's kernels may still read stage)
   Request D = R;
-  if (total <= kPackedMaxBytes && R.nsegs == 0 && R.num <= kLocalCap) {
-    // a single-launch sort reads and writes the columns in coherent host
-    // memory itself (no DMA commands: a small kernel's PCIe round trips cost
-    // less than two copy launches and their waits)
+  if (total <= kZeroCopyMaxBytes && R.nsegs == 0) {
+    // the kernels read and write the columns in coherent host memory
+    // themselves (no DMA commands: a small or mid-size sort's PCIe round
+    // trips cost less than two copy launches and their waits)
     for (int c = 0; c < R.ncols; c++) {
       memcpy(S->zc + off[c], R.in_cols[c], (size_t)R.num * col_width(R, c));
       D.in_cols[c] = D.out_cols[c] = S->zc + off[c];
