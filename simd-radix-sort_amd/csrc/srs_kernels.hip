@@ -4255,9 +4255,17 @@ void launch_key_hist(int key_size, int64_t n, const void* keys, const SortDesc& 
 
 // Kernel arguments are captured at launch, so the descriptor needs no pinned
 // staging buffer and is safe to rebuild for the next call immediately.
-__global__ void set_desc_kernel(SortDesc d, SortDesc* out) {
-  if (threadIdx.x == 0) *out = d;
+// The descriptor (~3.5 KB) copied by every thread of the block, a dword
+// each: as one lane's struct copy it took a few microseconds of the start
+// kernel's 8.5 (a 1M-key call is launch-bound)
+static_assert(sizeof(SortDesc) % 4 == 0, "dword copy of the descriptor");
+__device__ __forceinline__ void copy_desc(const SortDesc& d, SortDesc* out) {
+  const uint32_t* src = reinterpret_cast<const uint32_t*>(&d);
+  uint32_t* dst = reinterpret_cast<uint32_t*>(out);
+  for (uint32_t i = threadIdx.x; i < sizeof(SortDesc) / 4; i += blockDim.x) dst[i] = src[i];
 }
+
+__global__ void set_desc_kernel(SortDesc d, SortDesc* out) { copy_desc(d, out); }
 
 __device__ __forceinline__ void init_lists_body(Seg seg0, int to_local, Seg* big, Seg* local,
                                                 Seg* local2, ListCounters* ctr) {
@@ -4343,19 +4351,19 @@ void set_xcd_rotation(int mode) {
 }
 
 void launch_set_desc(const SortDesc& d, SortDesc* out, hipStream_t st) {
-  set_desc_kernel<<<1, 64, 0, st>>>(d, out);
+  set_desc_kernel<<<1, 256, 0, st>>>(d, out);
 }
 
 // set_desc + init_lists in one launch (a small sort is launch-bound)
 __global__ void start_kernel(SortDesc d, SortDesc* out, Seg seg0, int to_local, Seg* big,
                              Seg* local, Seg* local2, ListCounters* ctr) {
-  if (threadIdx.x == 0) *out = d;
+  copy_desc(d, out);
   init_lists_body(seg0, to_local, big, local, local2, ctr);
 }
 
 void launch_start(const SortDesc& d, SortDesc* out, Seg seg0, int to_local, Seg* big, Seg* local,
                   Seg* local2, ListCounters* ctr, hipStream_t st) {
-  start_kernel<<<1, 64, 0, st>>>(d, out, seg0, to_local, big, local, local2, ctr);
+  start_kernel<<<1, 256, 0, st>>>(d, out, seg0, to_local, big, local, local2, ctr);
 }
 
 
