@@ -2302,7 +2302,7 @@ int host_sort_single(Request& R, int dev) {
   hipStream_t st = S->st;
   WsUse use;
   SRS_TRY(use.begin(W, st));
-  HIP_TRY(hipStreamSynchronize(st));  // (the previous call's kernels may still read stage)
+  SRS_TRY(sync_poll(st));  // (the previous call's kernels may still read stage)
   Request D = R;
   if (total <= kZeroCopyMaxBytes && R.nsegs == 0) {
     // the kernels read and write the columns in coherent host memory
@@ -2340,7 +2340,7 @@ int host_sort_single(Request& R, int dev) {
     SRS_TRY(staged_copy(S, (char*)D.in_cols[c], (char*)R.in_cols[c],
                         (size_t)R.num * col_width(R, c), true));
   SRS_TRY(run_sort(W, D, st));
-  HIP_TRY(hipStreamSynchronize(st));
+  SRS_TRY(sync_poll(st));
   for (int c = 0; c < R.ncols; c++)
     SRS_TRY(staged_copy(S, (char*)D.out_cols[c], (char*)R.out_cols[c],
                         (size_t)R.num * col_width(R, c), false));
