@@ -461,7 +461,13 @@ def measure(cfg_name, args, torch, srs_amd, dist, dev, rank, world, shard):
             uid.copy_(torch.frombuffer(bytearray(shard_mod.unique_id()), dtype=torch.uint8))
         dist.broadcast(uid, 0)
         comm = shard_mod.ShardComm.rccl(world, rank, bytes(uid.cpu().numpy().tobytes()), dev)
-        comm.set_options(args.rounds, args.chunks)
+        rounds, chunks = args.rounds, args.chunks
+        if world == 1 and rounds == 0 and chunks == 0:
+            # the world-1 line exists to model the 8-GPU run (t8_model): it
+            # runs the plan the library uses at world > 1 (8 chunks, 16
+            # rounds), not world 1's own (one chunk: a 10 ms head)
+            rounds, chunks = 16, 8
+        comm.set_options(rounds, chunks)
     shard_out = []
 
     def step():
