@@ -66,9 +66,16 @@ def parse():
                     help="shard exchange rounds (srs_shard_set_options; 0 = library default)")
     ap.add_argument("--chunks", type=int, default=0,
                     help="shard partition chunks (srs_shard_set_options; 0 = library default)")
-    ap.add_argument("--t1-ms", type=float, default=21.245,
+    ap.add_argument("--t1-ms", type=float, default=None,
                     help="one-GPU step time the --shard world-1 line's 8-GPU model compares "
-                         "against (default: BENCH_r04's C1)")
+                         "against (default: measured in the same run: the plain sort of the "
+                         "same input, same steps)")
+    ap.add_argument("--self-messages", action="store_true",
+                    help="shard: own pieces as RCCL messages to the rank itself instead of "
+                         "device copies (srs_shard_set_message_options), so that world 1 runs "
+                         "every ncclSend / ncclRecv of the exchange")
+    ap.add_argument("--msg-cap-mb", type=float, default=0,
+                    help="shard: largest message in MiB (0 = the library's 256)")
     ap.add_argument("--alloc-steps", type=int, default=3,
                     help="world 1: extra steps with outputs from torch's allocator and in place "
                          "on a torch array (ms_per_step_plain_alloc / _inplace; 0 = skip)")
@@ -94,7 +101,7 @@ def parse():
 
 
 DISTS = ("uniform", "gaussian", "zero", "zeroone", "sorted", "reverse", "almostsorted",
-         "almostreverse")
+         "almostreverse", "span8")
 
 
 def make_dist_keys(keys, pays, dist, torch, srs_amd, kind):
@@ -103,7 +110,9 @@ def make_dist_keys(keys, pays, dist, torch, srs_amd, kind):
     Gaussian = round(N(0, 100)); Zero; ZeroOne; Sorted / ReverseSorted =
     uniform, sorted; Almost* = that plus 2^log10(n) random swaps. Sorting
     uses this library (the input of the timed sort is then its own output).
-    Payloads are recomputed as f(key)."""
+    span8 (not one of the reference's): uniform keys confined to 1/8 of the
+    key range (top 3 bits 001), the span one of 8 shard ranks receives
+    (DESIGN.md §7). Payloads are recomputed as f(key)."""
     import math
     n = keys.numel()
     g = torch.Generator(device=keys.device)
@@ -114,6 +123,10 @@ def make_dist_keys(keys, pays, dist, torch, srs_amd, kind):
         keys.zero_()
     elif dist == "zeroone":
         keys.copy_(torch.randint(0, 2, (n,), device=keys.device, generator=g))
+    elif dist == "span8":
+        for i in range(0, n, 1 << 26):
+            k = keys[i:i + (1 << 26)]
+            k.copy_(((k >> 3) & ((1 << 61) - 1)) | (1 << 61))
     elif dist in ("sorted", "reverse", "almostsorted", "almostreverse"):
         srs_amd.sort_device(keys, key_kind=kind, up=dist in ("sorted", "almostsorted"))
         if dist.startswith("almost"):
@@ -468,6 +481,7 @@ def measure(cfg_name, args, torch, srs_amd, dist, dev, rank, world, shard):
             # rounds), not world 1's own (one chunk: a 10 ms head)
             rounds, chunks = 16, 8
         comm.set_options(rounds, chunks)
+        comm.set_message_options(args.self_messages, int(args.msg_cap_mb * (1 << 20)) // 64 * 64)
     shard_out = []
 
     def step():
@@ -546,15 +560,22 @@ def measure(cfg_name, args, torch, srs_amd, dist, dev, rank, world, shard):
         # DESIGN.md §7 model's prediction
         rep = comm.report()
         mine = {"rank": rank, "chunks": rep["chunks"], "rounds": rep["rounds"],
+                "self_messages": rep.get("self_messages"), "sends": rep.get("sends"),
+                "recvs": rep.get("recvs"), "max_message_bytes": rep.get("max_message_bytes"),
+                "deferred_frees": rep.get("deferred_frees"),
                 "stamps_ms": rep["stamps_ms"],
                 "bytes_to_peer_per_round": rep["bytes_to_peer_per_round"],
                 **shard_mod.link_figures(rep)}
         if world == 1:
             # the head and tail measured here, in DESIGN.md §7's 8-GPU model
-            # (T(1) = the plain one-GPU step of the same shape, 21.2 ms for C1
-            # in BENCH_r04; pass --t1-ms to use another)
+            # against T(1) = the plain one-GPU sort of the same input in the
+            # same process (or --t1-ms)
+            t1 = args.t1_ms
+            if t1 is None:
+                t1 = plain_step_ms(keys, pays, kind, args.steps, torch, srs_amd)
+                mine["t1_ms_measured"] = round(t1, 3)
             mine["t8_model"] = shard_mod.t8_model(
-                mine.get("head_ms") or 0.0, mine.get("tail_ms") or 0.0, args.t1_ms, n=n,
+                mine.get("head_ms") or 0.0, mine.get("tail_ms") or 0.0, t1, n=n,
                 rec_bytes=rec_bytes)
         allph = [None] * world
         dist.all_gather_object(allph, mine)
@@ -646,6 +667,23 @@ def measure(cfg_name, args, torch, srs_amd, dist, dev, rank, world, shard):
         **alloc_ms,
         **({"phases": phases} if phases is not None else {}),
     }
+
+
+def plain_step_ms(keys, pays, kind, steps, torch, srs_amd):
+    """ms per plain one-GPU sort (out of place into srs_alloc_device outputs)
+    of the same resident input, as the headline line times it: the T(1) of
+    the world-1 shard line's 8-GPU model."""
+    ko = srs_amd.empty_device(keys.numel(), keys.dtype, keys.device).view(keys.shape)
+    po = [srs_amd.empty_device(p.numel(), p.dtype, p.device).view(p.shape) for p in pays]
+    srs_amd.sort_device(keys, *pays, key_kind=kind, out=(ko, *po))
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        srs_amd.sort_device(keys, *pays, key_kind=kind, out=(ko, *po))
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) / steps * 1e3
+    del ko, po
+    return ms
 
 
 def alloc_variants(args, step_args, torch, srs_amd):

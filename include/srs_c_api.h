@@ -237,6 +237,18 @@ int srs_shard_comm_init_staged(int32_t world, srs_shard_comm* comms);
  * fails every rank with SRS_ERR_INVALID_ARG). */
 int srs_shard_set_options(srs_shard_comm comm, int32_t rounds, int32_t chunks);
 
+/* Message options of later sorts on this communicator. self_messages = 1:
+ * this rank's own pieces travel as transport messages to itself (a send and
+ * a receive inside the round's group, as a peer's do) instead of device
+ * copies, so that one rank exercises every transport call of the exchange
+ * (the receive buffer then never aliases the partition buffer).
+ * max_message_bytes: the largest single message, a multiple of 64 in
+ * [64, 2^30]; 0 = the default 256 MiB (RCCL corrupts messages above 1 GiB,
+ * DESIGN.md §7). Every rank must use the same cap (checked like the options
+ * above); self messages are a rank's own choice. */
+int srs_shard_set_message_options(srs_shard_comm comm, int32_t self_messages,
+                                  int64_t max_message_bytes);
+
 /* This rank's part of the shard sort of device columns (inputs untouched):
  * *keys_out / payloads_out[k] receive device pointers to this rank's sorted
  * key range and *num_out its length; the memory belongs to the communicator
@@ -260,7 +272,10 @@ int srs_shard_sort_multi(int32_t num_devices, const srs_shard_comm* comms, const
  * rank, chunks, rounds, groups, records in / out, record bytes, "stamps_ms"
  * (HIP-event times since its start of: hist, plan, partition<c>,
  * round<r>_recv, round<r>_sort_start, round<r>_sort_end, end) and
- * "bytes_to_peer_per_round" ([round][peer] bytes this rank sent). */
+ * "bytes_to_peer_per_round" ([round][peer] bytes this rank sent; itself too
+ * with self messages), self_messages, max_message_bytes, sends / recvs (the
+ * transport calls posted) and deferred_frees (workspace buffers that grew
+ * during the exchange; their old memory is freed after it). */
 int srs_shard_last_report(srs_shard_comm comm, char* buf, int64_t cap);
 
 /* Test hook: the next sort on this communicator fails at `point` (0 = none,
@@ -271,7 +286,8 @@ int srs_shard_debug_inject(srs_shard_comm comm, int32_t point);
 
 /* The shard plan of one rank, host only (no GPU): from every rank's chunk
  * histograms (chunk_hists[src][chunk][2^min(12, key_bits)] of the
- * transformed top key bits) and this rank's record count, the JSON of
+ * transformed top key bits), this rank's record count and whether its own
+ * pieces travel as self messages (srs_shard_set_message_options), the JSON of
  * group_of_bin, rank_of_group, chunk_bounds, total (records received),
  * "posts" (every message group in posting order: its (round, chunk) pieces
  * and msgs = [op (0 send, 1 receive, 2 own-piece copy), peer, partitioned
@@ -279,8 +295,8 @@ int srs_shard_debug_inject(srs_shard_comm comm, int32_t point);
  * range, its sort segments and known top bits). The same code plans the
  * device sort; tests drive the protocol with it on CPU (gloo). */
 int srs_debug_shard_plan(int32_t world, int32_t rank, int32_t chunks, int32_t rounds,
-                         int32_t key_bits, const uint64_t* chunk_hists, int64_t num, char* json,
-                         int64_t cap);
+                         int32_t key_bits, int32_t self_messages, const uint64_t* chunk_hists,
+                         int64_t num, char* json, int64_t cap);
 
 /* ---- host arrays over several GPUs --------------------------------------- */
 

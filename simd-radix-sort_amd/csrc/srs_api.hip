@@ -443,10 +443,40 @@ void free_buf(DevBuf& b) {
   b = DevBuf();
 }
 
+std::mutex g_pub_amu;
+std::map<void*, size_t> g_pub_allocs;  // srs_alloc_device: base -> bytes
+
+// [p, p + bytes) lies inside one srs_alloc_device buffer (placement-probed)
+bool placed_memory(const void* p, size_t bytes) {
+  std::lock_guard<std::mutex> g(g_pub_amu);
+  auto it = g_pub_allocs.upper_bound(const_cast<void*>(p));
+  if (it == g_pub_allocs.begin()) return false;
+  --it;
+  const char* a = (const char*)it->first;
+  return (const char*)p >= a && (const char*)p + bytes <= a + it->second;
+}
+
+// While this thread runs the multi-GPU shard's exchange (srs_shard.hip),
+// workspace buffers that grow keep their old memory until the exchange is
+// over: hipFree waits for the whole device, i.e. for every receive already
+// queued on the communication stream -- without the transport's time limit,
+// and it would serialise the round sorts behind the exchange.
+thread_local bool t_defer = false;
+thread_local std::vector<std::pair<void*, int>> t_deferred;
+
+hipError_t ws_free(void* p, int mode) {
+  if (!p) return hipSuccess;
+  if (t_defer) {
+    t_deferred.push_back({p, mode});
+    return hipSuccess;
+  }
+  return big_free(p, mode);
+}
+
 int ensure(DevBuf& b, size_t bytes, int mode = ALLOC_MALLOC, bool placed = false) {
   if (b.bytes >= bytes && b.p) return SRS_OK;
   if (b.p) {
-    HIP_TRY(big_free(b.p, b.mode));
+    HIP_TRY(ws_free(b.p, b.mode));
     b.p = nullptr;
     b.bytes = 0;
   }
@@ -468,7 +498,7 @@ int ensure_keep(DevBuf& b, size_t bytes, size_t live_bytes, hipStream_t st) {
   if (b.p && live_bytes) HIP_TRY(hipMemcpyAsync(nb.p, b.p, live_bytes, hipMemcpyDeviceToDevice, st));
   if (b.p) {
     HIP_TRY(hipStreamSynchronize(st));
-    HIP_TRY(hipFree(b.p));
+    HIP_TRY(ws_free(b.p, ALLOC_MALLOC));
   }
   b = nb;
   return SRS_OK;
@@ -479,6 +509,15 @@ int ensure_keep(DevBuf& b, size_t bytes, size_t live_bytes, hipStream_t st) {
 // costs ~30 us per call (the mid-size measurements), several
 // times per sort; a level's kernels take a few ms at most, so the poll ends
 // the wait in ~1 us.
+// a spin-wait hint (x86 `pause`; elsewhere a yield)
+inline void cpu_relax() {
+#if defined(__x86_64__) || defined(__i386__)
+  __builtin_ia32_pause();
+#else
+  std::this_thread::yield();
+#endif
+}
+
 int sync_poll(hipStream_t st) {
   const auto t0 = std::chrono::steady_clock::now();
   for (;;) {
@@ -486,7 +525,7 @@ int sync_poll(hipStream_t st) {
     if (q == hipSuccess) return SRS_OK;
     if (q != hipErrorNotReady) HIP_TRY(q);
     if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(20)) break;
-    __builtin_ia32_pause();
+    cpu_relax();
   }
   HIP_TRY(hipStreamSynchronize(st));
   return SRS_OK;
@@ -506,6 +545,8 @@ struct Workspace {
   DevBuf prun, ptile, btot, bnt, btile, nt_over, gtile, gorder;
   int64_t gorder_cap = 0;
   DevBuf mid;  // mid-size single launch: the tiles' key OR / AND, their digit counts
+  DevBuf midbar;  // and its grid barriers' arrival words (zeroed once)
+  unsigned long long midbar_base = 0;  // arrivals so far on each of them
   ListCounters* h_ctr = nullptr;
   uint64_t* h_totals = nullptr;
   MidFlag* h_mid = nullptr;        // the mid-size launch's early answer
@@ -538,7 +579,7 @@ struct Workspace {
                       &fallback2, &redo, &redo2, &shist, &lut, &lut_rbits, &copy, &plan, &tcount,
                       &gcount, &tbase, &gbase, &var, &sbase, &tile_seg, &group_seg, &hist, &offs,
                       &gsum, &gofs, &scan_tmp, &totals, &ctr, &prun, &ptile, &btot, &bnt, &btile,
-                      &nt_over, &gtile, &gorder, &mid};
+                      &nt_over, &gtile, &gorder, &mid, &midbar};
     for (DevBuf* b : bufs) free_buf(*b);
     for (auto& t : small_taken) free_buf(t.second);
     if (h_ctr) (void)hipHostFree(h_ctr);
@@ -1191,7 +1232,7 @@ int plan_balanced_level(Workspace* W, const Request& R, const SortDesc& d, bool*
 // small digit tables with 4-byte keys, AoS records from the second level on.
 // SRS_PAIR_TILES (A/B runs): 0 off, 1 every plain-digit level, 3 every
 // supported level, 2 (or unset) the default.
-int pair_tiles_mode(const SortDesc& d, int ks) {
+int pair_tiles_mode(const SortDesc& d, int ks, bool aos_slices) {
   const char* e = getenv("SRS_PAIR_TILES");
   const int mode = e && *e ? atoi(e) : 2;
   if (mode == 0 || d.canon_zero || (ks != 4 && ks != 8)) return 0;
@@ -1202,7 +1243,6 @@ int pair_tiles_mode(const SortDesc& d, int ks) {
   if (!shape) return 0;
   if (mode == 3) return 1 | 2;
   if (mode == 1) return 1;
-  const bool aos_slices = d.tmp2 && !d.pair;
   return aos_slices ? (1 | 4) : ks == 4 ? (1 | 2) : 1;
 }
 
@@ -1492,10 +1532,12 @@ int run_small(Workspace* W, const Request& R, hipStream_t st) {
 bool direct_layout_ok(const SortDesc& d, int pm, int ks) {
   const Col& k = d.cols[0];
   const int bufs[] = {BUF_IN, BUF_OUT, BUF_TMP, BUF_TMP2};
-  if (pm == 0) {
-    if (d.ncols != 2 || d.tmp2 || d.cols[1].width != 8 || k.width != (uint32_t)ks) return false;
-    for (int b : {BUF_IN, BUF_OUT, BUF_TMP})
+  if (pm == 0) {  // (TMP2: the home-write layout, dense SoA columns too)
+    if (d.ncols != 2 || d.pair || d.cols[1].width != 8 || k.width != (uint32_t)ks) return false;
+    for (int b : {BUF_IN, BUF_OUT, BUF_TMP, BUF_TMP2}) {
+      if (b == BUF_TMP2 && !d.tmp2) continue;
       if (k.stride[b] != k.width || d.cols[1].stride[b] != 8) return false;
+    }
     return true;
   }
   if (pm == 1) {
@@ -1626,8 +1668,20 @@ int plan_range_level(Workspace* W, const Request& R, const std::vector<KeyCluste
 
 int copy_through(const Request& R, hipStream_t st);
 
-// Mid-size sorts (kLocalCap < n <= kMidMaxKeys) take one cooperative launch
+// Mid-size sorts (kLocalCap < n <= kMidMaxKeys) take one launch with grid barriers
 // (launch_mid_sort); SRS_MID=0 sends them down the general path.
+// (below this a sort's columns stay in the L2 / Infinity Cache and the
+// placement of OUT does not matter)
+constexpr int64_t kHomeTmp2MinN = int64_t(1) << 24;
+
+bool home_tmp2_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("SRS_HOME_TMP2");
+    return !(e && *e == '0');
+  }();
+  return on;
+}
+
 bool mid_enabled() {
   static const bool on = [] {
     const char* e = getenv("SRS_MID");
@@ -1647,7 +1701,7 @@ int wait_mid_flag(const MidFlag* f, unsigned long long seq, hipStream_t st) {
       if (!seen()) return fail(SRS_ERR_INTERNAL, "mid-size launch: no answer from the kernel");
       break;
     }
-    __builtin_ia32_pause();
+    cpu_relax();
   }
   return SRS_OK;
 }
@@ -1686,6 +1740,19 @@ int run_sort(Workspace* W, const Request& R, hipStream_t st) {
   // 23.6 -> 21.1 ms at 1e9)
   const bool pair_cols = !R.aos && R.ncols == 3 && R.widths[1] == 4 && R.widths[2] == 4 &&
                          n > kLocalCap && R.nsegs == 0 && !mid;
+  // Home write (round 6): when the output columns are not placement-probed
+  // memory (srs_alloc_device) -- the reference's in-place contract
+  // (radixSort.hpp:1780) on the caller's own array, or any array of the
+  // caller's allocator -- the scatters stay in the workspace (IN -> TMP ->
+  // TMP2, both placed) and only the local pass writes OUT, as one
+  // contiguous run per segment. The scatter's partial 64-byte blocks are
+  // what an unlucky placement slows down (6.2 vs 7.0 ms per
+  // launch); a streaming write is far less exposed. (SRS_HOME_TMP2=0: off)
+  bool home_tmp2 = false;
+  if (!R.aos && !pair_cols && n >= kHomeTmp2MinN && R.nsegs == 0 && !mid && home_tmp2_enabled()) {
+    for (int c = 0; c < R.ncols && !home_tmp2; c++)
+      home_tmp2 = !placed_memory(R.out_cols[c], (size_t)n * R.widths[c]);
+  }
   size_t tmp_bytes = 0, slice_bytes = 0;
   std::vector<size_t> tmp_off;
   if (R.aos) {
@@ -1701,7 +1768,11 @@ int run_sort(Workspace* W, const Request& R, hipStream_t st) {
   SRS_TRY(ensure(W->tmp, tmp_bytes, ws_alloc_mode(), true));
   char* tmp = (char*)W->tmp.p;
   char* tmp2 = nullptr;
-  if (aos_cols || pair_cols) {
+  if (home_tmp2 && ensure(W->tmp2, tmp_bytes, ws_alloc_mode(), true) != SRS_OK) {
+    home_tmp2 = false;  // (no room for TMP2: the scatter writes OUT as before)
+    (void)hipGetLastError();
+  }
+  if (aos_cols || pair_cols || home_tmp2) {
     SRS_TRY(ensure(W->tmp2, tmp_bytes, ws_alloc_mode(), true));
     tmp2 = (char*)W->tmp2.p;
     d.tmp2 = 1;
@@ -1788,11 +1859,18 @@ int run_sort(Workspace* W, const Request& R, hipStream_t st) {
   } else {
     bool started = false;  // (by the mid-size launch)
     if (mid) {
-      // one cooperative launch: the first level and every bucket's local
+      // one launch (grid barriers): the first level and every bucket's local
       // sort; buckets over kLocalCap (skewed keys) come back in the big list
       // and continue on the general levels below
       const int64_t T = (n + kTile - 1) / kTile;
       SRS_TRY(ensure(W->mid, T * 16 + T * kMaxBins * sizeof(uint32_t)));
+      if (!W->midbar.p) {
+        SRS_TRY(ensure(W->midbar, mid_bar_words() * sizeof(unsigned long long)));
+        HIP_TRY(hipMemsetAsync(W->midbar.p, 0, mid_bar_words() * sizeof(unsigned long long), st));
+      }
+      auto barrier_failed = [&] { return __atomic_load_n(&W->h_mid->err, __ATOMIC_ACQUIRE) != 0; };
+      if (barrier_failed())  // (an earlier call's barrier timed out: its output was wrong)
+        return fail(SRS_ERR_INTERNAL, "mid-size launch: a grid barrier timed out");
       DevBuf* tk = nullptr;
       SRS_TRY(taken_slot(W, st, &tk));
       DevBuf& taken = *tk;
@@ -1803,11 +1881,12 @@ int run_sort(Workspace* W, const Request& R, hipStream_t st) {
         TimedScope ts("mid", (double)0, st);
         e = launch_mid_sort(ksl, d, n, home, (unsigned long long*)W->mid.p,
                             (uint32_t*)((char*)W->mid.p + T * 16), d_ctr, (Seg*)W->big[0].p,
-                            (unsigned long long*)taken.p, W->h_mid, seq, st);
+                            (unsigned long long*)taken.p, W->h_mid, seq,
+                            (unsigned long long*)W->midbar.p, &W->midbar_base, st);
       }
       if (e != hipSuccess) {
-        // (a cooperative launch the device cannot take: the general path,
-        // which the column layout chosen for `mid` also serves)
+        // (a grid the device cannot hold resident: the general path, which
+        // the column layout chosen for `mid` also serves)
         (void)hipGetLastError();
         if (trace_levels())
           fprintf(stderr, "[srs] mid-size launch refused (%s): general path\n", hipGetErrorString(e));
@@ -1816,6 +1895,8 @@ int run_sort(Workspace* W, const Request& R, hipStream_t st) {
         // once the first level's sizes are known (MidFlag): polled for a
         // while (a stream sync's wake-up cost ~30 us per call), then waited for
         SRS_TRY(wait_mid_flag(W->h_mid, seq, st));
+        if (barrier_failed())
+          return fail(SRS_ERR_INTERNAL, "mid-size launch: a grid barrier timed out");
         const unsigned long long nb_flag = __atomic_load_n(&W->h_mid->n_big, __ATOMIC_ACQUIRE);
         if (nb_flag >> 63)
           return fail(SRS_ERR_INTERNAL, "mid-size launch: more buckets than workgroups");
@@ -1844,7 +1925,7 @@ int run_sort(Workspace* W, const Request& R, hipStream_t st) {
     }
   }
   LevelState S{n_big, n_local, n_local2, n_copy, 0, d.ncols, d.tmp2};
-  S.pair_tiles = pair_tiles_mode(d, ks);
+  S.pair_tiles = pair_tiles_mode(d, ks, aos_cols);
   if (R.nsegs == 0 && n_big == 1 && !mid_continued) S.known_len = n;
   int level = 0;
   // Stripe first level: large plain SoA sorts partition
@@ -1938,7 +2019,7 @@ int run_sort(Workspace* W, const Request& R, hipStream_t st) {
       // 1 16-byte records of an 8-byte key as slices (C3), 2 a key + two
       // 4-byte payloads (C2)
       int pm = -1;
-      if (!R.aos && R.ncols == 2 && R.widths[1] == 8 && !d.tmp2) pm = 0;
+      if (!R.aos && R.ncols == 2 && R.widths[1] == 8 && !d.pair) pm = 0;
       else if (rec16 && ks == 8) pm = 1;
       else if (d.pair && ks == 4) pm = 2;
       if (pm >= 0 && !direct_layout_ok(d, pm, ks)) pm = -1;  // (the kernel assumes it)
@@ -2715,6 +2796,18 @@ int set_leaf_mode(Request& R, int leaf_mode) {
 // (other translation units of the library report errors through this)
 int set_error(int code, const std::string& msg) { return fail(code, msg); }
 
+void defer_workspace_frees(bool on) { t_defer = on; }
+
+// Frees what defer_workspace_frees held back (the caller's exchange is over);
+// returns how many buffers that was.
+int64_t release_deferred_frees() {
+  std::vector<std::pair<void*, int>> v;
+  v.swap(t_deferred);
+  for (auto& f : v) (void)big_free(f.first, f.second);
+  (void)hipGetLastError();
+  return (int64_t)v.size();
+}
+
 // Grows the current device's workspace so that a later
 // srs_sort_segments_device of up to `num` records of these column widths
 // allocates no large buffer: the multi-GPU shard reserves it before its first
@@ -3060,9 +3153,6 @@ int srs_debug_plan_table(const uint32_t* hist, int64_t num, int key_bits, int32_
   if (P.mode) memcpy(rbits, P.rbits.data(), kGroups * 4);
   return SRS_OK;
 }
-
-std::mutex g_pub_amu;
-std::map<void*, size_t> g_pub_allocs;  // srs_alloc_device
 
 int srs_alloc_device(uint64_t bytes, void** ptr) {
   if (!ptr) return fail(SRS_ERR_INVALID_ARG, "srs_alloc_device: ptr is NULL");

@@ -123,6 +123,7 @@ constexpr int kStripeKeysPerBucket = SRS_STRIPE_KPB;
 struct MidFlag {
   unsigned long long n_big;  // buckets handed back to the general levels (bit 63: error)
   unsigned long long seq;    // the call's sequence number
+  unsigned long long err;    // the seq of a call whose grid barrier timed out (0: none)
 };
 
 // Work-list counters (device), read back by the host once per level.

@@ -15,11 +15,11 @@
 //
 // All kernels are integer byte movement (no MFMA); the roofline is HBM.
 // wave64 everywhere; __ballot returns 64-bit masks.
-#include <hip/hip_cooperative_groups.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include <algorithm>
+#include <atomic>
 #include <type_traits>
 
 #include "srs_common.h"
@@ -2219,7 +2219,8 @@ __device__ __forceinline__ bool local_fast_body(const SortDesc* __restrict__ des
     // load or store path)
     const bool direct = !CZ && !wide && desc->cols[0].width == (uint32_t)kbytes &&
                         desc->cols[0].stride[BUF_OUT] == (uint32_t)kbytes &&
-                        (!desc->tmp2 || desc->pair) &&
+                        (!desc->tmp2 || desc->pair ||
+                         desc->cols[0].stride[BUF_TMP2] == (uint32_t)kbytes) &&
                         desc->cols[0].stride[BUF_IN] == (uint32_t)kbytes;
     auto bucket_rank = [&](auto DIRECT_) -> bool {
     constexpr bool DIRECT = decltype(DIRECT_)::value;
@@ -3443,7 +3444,7 @@ __global__ __launch_bounds__(NT) void small_sort_kernel(const SortDesc d, const 
 // Between one workgroup's small sort and the general path (a plan, a count,
 // three offset kernels and a scatter per level, then the local kernels:
 // about twelve dependent launches, ~85 us of GPU-side span at 8K-64K keys,
-// almost all of it launch gaps) one cooperative launch of G = ceil(n / 4096)
+// almost all of it launch gaps) one launch of G = ceil(n / 4096)
 // workgroups does it all, with grid barriers between the phases:
 //   1. every workgroup loads its tile and reduces the keys' OR / AND;
 //   2. the global varying bits give the digit (choose_bits, as a level
@@ -3459,7 +3460,7 @@ __global__ __launch_bounds__(NT) void small_sort_kernel(const SortDesc d, const 
 // one bucket each, no loop -- a loop over buckets had the compiler hoist the
 // bodies' per-thread invariants out of it and spill 55 VGPRs. One
 // workgroup per CU (129 KB of LDS), so G must fit the chip for the
-// cooperative launch.
+// launch (its grid barriers need every workgroup resident).
 constexpr int kMidMaxTiles = 64;  // n <= 262144
 constexpr int kMidMat = 8192;     // tiles x buckets (64 x 128 at kMidMaxKeys)
 static_assert(kMidMat % kScatterThreads == 0, "count matrix: whole rounds of loads");
@@ -3471,6 +3472,45 @@ struct MidLevelLds {
   uint32_t hist[kMaxBins];
   uint32_t mat[kMidMat];  // every tile's bucket counts (phase 3)
 };
+
+// A grid barrier of the mid-size launch. Every workgroup is resident (the
+// host launches G <= CUs x resident workgroups per CU, one per CU at 129 KB
+// of LDS), so a plain launch with arrival counters replaces the cooperative
+// launch (processes that had made a cooperative launch crashed
+// in the runtime's teardown at exit under rocprofv3). Barrier k counts on its
+// own 64-bit word, which only ever grows: every call passes each of its
+// three barriers once with all G workgroups, so the host knows the count
+// before the call (`base`, the sum of the earlier calls' G) and a barrier is
+// full at base + G; no reset between calls (they are stream-ordered on the
+// workspace). One atomic add per workgroup: a compare-and-swap arrival
+// (tagged words) serialised 128 workgroups' retries, 0.6 ms per call. The
+// agent-scope fences write this workgroup's stores back to the shared point
+// of coherence before it arrives and invalidate stale lines after the wait
+// (workgroups sit on different XCDs, each with its own L2). The wait is
+// bounded: a barrier that never fills (it cannot, short of a broken
+// residency assumption) posts the call's seq to MidFlag::err and lets the
+// grid drain instead of hanging the GPU; the host checks it.
+constexpr int kMidBarWords = 3;
+__device__ __forceinline__ void mid_grid_barrier(unsigned long long* bar, int k,
+                                                 unsigned long long full, unsigned long long seq,
+                                                 MidFlag* flag) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long* w = bar + k;
+    __threadfence();  // (release: this workgroup's global writes)
+    __hip_atomic_fetch_add(w, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (uint32_t spin = 0;
+         __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < full; spin++) {
+      __builtin_amdgcn_s_sleep(2);
+      if (spin > (1u << 24)) {  // (seconds: never in a correct run)
+        __hip_atomic_store(&flag->err, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+    }
+    __threadfence();  // (acquire: the other workgroups' writes)
+  }
+  __syncthreads();
+}
 
 __device__ __forceinline__ void mid_tell_host(MidFlag* f, unsigned long long n_big,
                                               unsigned long long seq) {
@@ -3486,10 +3526,10 @@ template <typename KT, typename U, bool CZ>
 __global__ __launch_bounds__(kLocalThreads) void mid_sort_kernel(
     const SortDesc d, int64_t n, int32_t src, unsigned long long* __restrict__ part,
     uint32_t* __restrict__ hist, ListCounters* __restrict__ ctr, Seg* __restrict__ big,
-    unsigned long long* __restrict__ taken, MidFlag* __restrict__ flag, unsigned long long seq) {
+    unsigned long long* __restrict__ taken, MidFlag* __restrict__ flag, unsigned long long seq,
+    unsigned long long* __restrict__ bar, unsigned long long bar_base) {
+  const unsigned long long full = bar_base + gridDim.x;  // (every barrier of this call)
   static_assert(kLocalThreads == kScatterThreads, "the level phases use the scatter's shape");
-  namespace cg = cooperative_groups;
-  cg::grid_group grid = cg::this_grid();
   __shared__ MidLds Ls;
   __shared__ int64_t my_start;
   __shared__ int32_t my_len;
@@ -3550,7 +3590,7 @@ __global__ __launch_bounds__(kLocalThreads) void mid_sort_kernel(
     *ctr = ListCounters{};
     taken[0] = taken[1] = 0;
   }
-  grid.sync();
+  mid_grid_barrier(bar, 0, full, seq, flag);
 
   // ---- 2. the digit; this tile's counts
   // (the T pairs in one round of loads: a loop over them paid a cross-XCD
@@ -3590,7 +3630,11 @@ __global__ __launch_bounds__(kLocalThreads) void mid_sort_kernel(
                         desc->cols[c].stride[BUF_OUT], tbase, ebase, cnt,
                         [&](int k) { return t[k]; });
       }
-    return;  // (uniform over the grid: no barrier follows)
+    // (uniform over the grid; the later barriers are still passed, so that
+    // every call adds G to each barrier word)
+    mid_grid_barrier(bar, 1, full, seq, flag);
+    mid_grid_barrier(bar, 2, full, seq, flag);
+    return;
   }
   const int rbits = 64 - __clzll((long long)var);
   const int bits = choose_bits(n, rbits);
@@ -3607,7 +3651,7 @@ __global__ __launch_bounds__(kLocalThreads) void mid_sort_kernel(
     for (uint32_t b = threadIdx.x; b < nb; b += kScatterThreads)
       hist[(size_t)w * kMaxBins + b] = Ls.level.hist[b];
   }
-  grid.sync();
+  mid_grid_barrier(bar, 1, full, seq, flag);
 
   // ---- 3. offsets; the stable scatter of the tile into TMP
   {
@@ -3669,7 +3713,7 @@ __global__ __launch_bounds__(kLocalThreads) void mid_sort_kernel(
                                                  v1, v2, my_off, DigitLut{});
     }
   }
-  grid.sync();
+  mid_grid_barrier(bar, 2, full, seq, flag);
 
   // ---- 4. bucket w, into OUT
   const int32_t len = my_len;
@@ -4124,20 +4168,48 @@ void launch_local_lsd(int key_size, const SortDesc* d, const Seg* segs,
 #undef CALL
 }
 
+int mid_bar_words() { return kMidBarWords; }
+
 hipError_t launch_mid_sort(int key_size, const SortDesc& d, int64_t n, int src,
                            unsigned long long* part, uint32_t* hist, ListCounters* ctr, Seg* big,
                            unsigned long long* taken, MidFlag* flag, unsigned long long seq,
-                           hipStream_t st) {
+                           unsigned long long* bar, unsigned long long* bar_base, hipStream_t st) {
   const unsigned T = (unsigned)((n + kTile - 1) / kTile);
   const unsigned nb_max = 1u << choose_bits(n, 64);
   if (T > (unsigned)kMidMaxTiles || T * nb_max > (unsigned)kMidMat) return hipErrorInvalidValue;
   const unsigned G = std::max(T, nb_max);  // (one bucket per workgroup)
-  SortDesc dd = d;
-  int32_t s32 = src;
-  void* args[] = {&dd, &n, &s32, &part, &hist, &ctr, &big, &taken, &flag, &seq};
+  // every workgroup must be resident at once (the grid barriers): G within
+  // the device's CUs x the kernel's resident workgroups per CU, else the
+  // caller takes the general path (e.g. a partition of a few CUs). Cached
+  // per device and key dispatch (the query costs microseconds per call).
+  static std::atomic<int> cap_cache[64][4];  // 0: not queried yet
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return hipErrorInvalidValue;
+  const int slot = (key_size & SRS_KS_CANON) ? 3 : (key_size & 0xff) >= 8 ? 2 : (key_size & 0xff) >= 4 ? 1 : 0;
+  int resident = cap_cache[dev][slot].load(std::memory_order_relaxed);
+  if (resident == 0) {
+    int cus = 0, per_cu = 0;
+    hipError_t oe = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+#define OCC(KT, U, CZ)                                                                            \
+  if (oe == hipSuccess)                                                                          \
+    oe = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, mid_sort_kernel<KT, U, CZ>,       \
+                                                      kLocalThreads, 0)
+    SRS_KEY_DISPATCH(key_size, OCC)
+#undef OCC
+    if (oe != hipSuccess) return oe;
+    resident = std::max(1, cus * per_cu);  // (>= 1: "queried")
+    if (per_cu < 1) resident = -1;
+    cap_cache[dev][slot].store(resident, std::memory_order_relaxed);
+  }
+  if (resident < 0 || (int64_t)G > (int64_t)resident) return hipErrorCooperativeLaunchTooLarge;
 #define CALL(KT, U, CZ)                                                                         \
-  return hipLaunchCooperativeKernel((const void*)mid_sort_kernel<KT, U, CZ>, dim3(G),          \
-                                    dim3(kLocalThreads), args, 0, st)
+  mid_sort_kernel<KT, U, CZ><<<G, kLocalThreads, 0, st>>>(d, n, src, part, hist, ctr, big,    \
+                                                          taken, flag, seq, bar, *bar_base);   \
+  {                                                                                           \
+    const hipError_t le_ = hipGetLastError();                                                 \
+    if (le_ == hipSuccess) *bar_base += G; /* (the launch's arrivals per barrier word) */     \
+    return le_;                                                                               \
+  }
   SRS_KEY_DISPATCH(key_size, CALL)
 #undef CALL
   return hipErrorInvalidValue;

@@ -61,6 +61,10 @@
 namespace srs {
 int set_error(int code, const std::string& msg);                                  // (srs_api.hip)
 int reserve_segments_workspace(int64_t num, int ncols, const uint32_t* widths);  // (srs_api.hip)
+// workspace frees of this thread held back while peers' messages are queued
+// on the device (a hipFree would wait for them, unbounded); srs_api.hip
+void defer_workspace_frees(bool on);
+int64_t release_deferred_frees();
 
 namespace {
 
@@ -145,8 +149,9 @@ constexpr int kMaxRounds = 64;                   // exchange rounds
 constexpr int kDefaultChunks = 8;                // (world > 1; world 1: one chunk)
 constexpr int kDefaultRounds = 16;               // (world > 1; world 1: 8)
 constexpr int kDefaultRounds1 = 8;
-constexpr int kHdr = 16;                         // header slots after the histogram
-constexpr size_t kMsgBytes = size_t(256) << 20;  // largest message
+constexpr int kHdr = 18;                         // header slots after the histogram
+constexpr size_t kMsgBytes = size_t(256) << 20;  // largest message (default)
+constexpr int64_t kMsgBytesMax = int64_t(1) << 30;  // RCCL corrupts larger ones
 
 double timeout_s() {
   const char* e = getenv("SRS_SHARD_TIMEOUT_S");
@@ -504,8 +509,9 @@ struct ShardPlan {
   std::vector<int64_t> soff;              // [chunk][group + 1] partitioned offsets
   int64_t total = 0;
   bool alias = false;                     // one rank, one chunk: receive = partition buffer
+  bool self = false;                      // own pieces as messages to this rank (not copies)
 
-  void init(int world, int rank, int chunks, int rounds, int key_bits) {
+  void init(int world, int rank, int chunks, int rounds, int key_bits, bool self_msgs = false) {
     w = world;
     me = rank;
     CH = chunks;
@@ -514,7 +520,8 @@ struct ShardPlan {
     bits = std::min(kBits, kbits);
     nb = 1 << bits;
     G = std::min(kGroups, nb);
-    alias = w == 1 && CH == 1;
+    self = self_msgs;
+    alias = w == 1 && CH == 1 && !self;
   }
   void split(const uint64_t* tot) {
     gob = balanced_split(tot, nb, G);
@@ -582,18 +589,19 @@ struct ShardPlan {
     }
   }
   // the messages of (round r, chunk c), in posting order: per peer, the
-  // send then the receive; this rank's own piece last (a device copy)
+  // send then the receive; this rank's own piece last (a device copy), or,
+  // with self messages, a send and a receive to itself in rank order
   std::vector<Msg> messages(int r, int c) const {
     std::vector<Msg> out;
     for (int d = 0; d < w; d++) {
       int gs;
-      if (d == me) continue;
+      if (d == me && !self) continue;
       const int64_t scnt = piece(me, c, d, r, &gs);
       if (scnt) out.push_back(Msg{0, d, soff[(size_t)c * (G + 1) + gs], 0, scnt});
       const int64_t rcnt = piece(d, c, me, r, &gs);
       if (rcnt) out.push_back(Msg{1, d, 0, roff[((size_t)r * w + d) * CH + c], rcnt});
     }
-    if (!alias) {
+    if (!alias && !self) {
       int gs;
       const int64_t cnt = piece(me, c, me, r, &gs);
       if (cnt)
@@ -638,11 +646,12 @@ struct ShardPlan {
       *known = shared_bits(lo, hi);
     }
   }
-  // records this rank sends each peer in round r
+  // records this rank sends each peer in round r (itself too with self
+  // messages)
   std::vector<int64_t> sent(int r) const {
     std::vector<int64_t> s(w, 0);
     for (int d = 0; d < w; d++) {
-      if (d == me) continue;
+      if (d == me && !self) continue;
       for (int c = 0; c < CH; c++) {
         int gs;
         s[d] += piece(me, c, d, r, &gs);
@@ -711,6 +720,8 @@ struct srs_shard_comm_s {
   std::unique_ptr<Transport> tr;
   int world = 1, rank = 0, device = 0;
   int rounds = 0, chunks = 0;  // 0: the defaults
+  int self_msgs = 0;           // srs_shard_set_message_options: own pieces as self messages
+  int64_t msg_cap = 0;         // largest message in bytes (0: kMsgBytes)
   int inject = 0;              // srs_shard_debug_inject (one sort)
   hipStream_t cs = nullptr;    // communication stream
   hipStream_t ss = nullptr;    // round sorts
@@ -721,6 +732,9 @@ struct srs_shard_comm_s {
   // the last sort, for srs_shard_last_report
   int last_chunks = 0, last_rounds = 0, last_groups = 0, last_rec_bytes = 0, last_ok = 0;
   int64_t last_in = 0, last_out = 0;
+  int last_self = 0;
+  int64_t last_cap = 0, last_sends = 0, last_recvs = 0;  // message cap, transport calls posted
+  int64_t last_deferred = 0;  // workspace frees held back during the exchange
   std::vector<std::vector<int64_t>> last_sent;  // [round][peer] records
   std::mutex mu;
 };
@@ -784,12 +798,14 @@ int shard_sort(srs_shard_comm C, int64_t n, int kind, int up, const void* keys, 
   const int kbits = 8 * ks;
   const int CH = C->chunks > 0 ? C->chunks : (w > 1 ? kDefaultChunks : 1);
   const int R = C->rounds > 0 ? C->rounds : (w > 1 ? kDefaultRounds : kDefaultRounds1);
+  const bool selfm = C->self_msgs != 0;
+  const size_t cap = C->msg_cap > 0 ? (size_t)C->msg_cap : kMsgBytes;
   const int ncols = 1 + np;
   std::vector<uint32_t> width(ncols);
   width[0] = (uint32_t)ks;
   for (int c = 0; c < np; c++) width[1 + c] = psz[c];
   ShardPlan P;
-  P.init(w, me, CH, R, kbits);
+  P.init(w, me, CH, R, kbits, selfm);
   const int nb = P.nb, G = P.G;
   if (err) n = 0;
   std::vector<int64_t> cb(CH + 1);
@@ -828,13 +844,23 @@ int shard_sort(srs_shard_comm C, int64_t n, int kind, int up, const void* keys, 
   put(9, (uint64_t)CH);
   put(11, (uint64_t)R);
   hs[13] = 1;
-  hs[14] = err ? 1ull << std::min(me, 63) : 0;
+  hs[14] = err ? 1ull << std::min(me, 63) : 0;  // (names the ranks; hs[0] counts them)
+  put(15, (uint64_t)(cap / 64));
   C->clk.stamp("hist", st);
   uint64_t* dH = (uint64_t*)C->hdr.p;
+  // (every read-back of a collective's result waits for the collective with
+  // the transport's bounded wait first: a device-to-host copy into pageable
+  // memory would block the host inside the copy, unbounded, on a peer that
+  // never joins)
+  auto read_back = [&](void* host, const void* dev, size_t bytes) -> int {
+    int rc = T.wait(st);
+    if (rc == SRS_OK) rc = hip_rc(hipMemcpyAsync(host, dev, bytes, hipMemcpyDeviceToHost, st), "read-back");
+    if (rc == SRS_OK) rc = hip_rc(hipStreamSynchronize(st), "read-back");  // (local work only)
+    return rc;
+  };
   SH_ABORT(hip_rc(hipMemcpyAsync(dH, H.data(), H.size() * 8, hipMemcpyHostToDevice, st), "header"));
   SH_ABORT(T.all_reduce_sum(dH, H.size(), st));
-  SH_ABORT(hip_rc(hipMemcpyAsync(H.data(), dH, H.size() * 8, hipMemcpyDeviceToHost, st), "header"));
-  SH_ABORT(T.wait(st));
+  SH_ABORT(read_back(H.data(), dH, H.size() * 8));
   if (hs[0]) {
     if (err) return set_error(err, emsg);
     return set_error(SRS_ERR_INVALID_ARG, "shard: rank(s) " + rank_list(hs[14]) +
@@ -842,9 +868,11 @@ int shard_sort(srs_shard_comm C, int64_t n, int kind, int up, const void* keys, 
   }
   if (hs[13] != (uint64_t)w) return set_error(SRS_ERR_INTERNAL, "shard: world size mismatch");
   static const char* what[] = {"key kind", "direction", "payload count", "payload sizes",
-                               "chunks (srs_shard_set_options)", "rounds (srs_shard_set_options)"};
-  for (int i = 0; i < 6; i++) {
-    const uint64_t s = hs[1 + 2 * i], q = hs[2 + 2 * i];
+                               "chunks (srs_shard_set_options)", "rounds (srs_shard_set_options)",
+                               "message cap (srs_shard_set_message_options)"};
+  static const int slot[] = {1, 3, 5, 7, 9, 11, 15};  // (13: the world count, 14: failing ranks)
+  for (int i = 0; i < 7; i++) {
+    const uint64_t s = hs[slot[i]], q = hs[slot[i] + 1];
     if ((uint64_t)w * q != s * s)
       return set_error(SRS_ERR_INVALID_ARG, std::string("shard: the ranks disagree on the ") +
                                                 what[i] + "; every rank must pass the same");
@@ -857,9 +885,7 @@ int shard_sort(srs_shard_comm C, int64_t n, int kind, int up, const void* keys, 
   std::vector<int64_t> mat((size_t)w * CH * G);
   SH_ABORT(hip_rc(hipMemcpyAsync(dcc, cc.data(), cc.size() * 8, hipMemcpyHostToDevice, st), "sizes"));
   SH_ABORT(T.all_gather(dcc, dcc + cc.size(), cc.size(), st));
-  SH_ABORT(hip_rc(hipMemcpyAsync(mat.data(), dcc + cc.size(), mat.size() * 8,
-                                 hipMemcpyDeviceToHost, st), "sizes"));
-  SH_ABORT(T.wait(st));
+  SH_ABORT(read_back(mat.data(), dcc + cc.size(), mat.size() * 8));
   P.layout(mat.data(), n);
 
   // 3. every buffer before the first message; one status for all ranks
@@ -877,15 +903,16 @@ int shard_sort(srs_shard_comm C, int64_t n, int kind, int up, const void* keys, 
   }
   if (!err) note(hip_rc(hipMemcpyAsync(C->lut.p, P.gob.data(), (size_t)nb * 4,
                                        hipMemcpyHostToDevice, st), "hipMemcpyAsync"));
+  // status: {failing ranks, their bits} (the count decides: a sum of bits
+  // could wrap beyond 64 ranks; the bits only name the ranks)
   uint64_t* dflag = (uint64_t*)C->flag.p;
-  uint64_t mask = err ? 1ull << std::min(me, 63) : 0;
-  SH_ABORT(hip_rc(hipMemcpyAsync(dflag, &mask, 8, hipMemcpyHostToDevice, st), "status"));
-  SH_ABORT(T.all_reduce_sum(dflag, 1, st));
-  SH_ABORT(hip_rc(hipMemcpyAsync(&mask, dflag, 8, hipMemcpyDeviceToHost, st), "status"));
-  SH_ABORT(T.wait(st));
-  if (mask) {
+  uint64_t stat[2] = {err ? 1ull : 0ull, err ? 1ull << std::min(me, 63) : 0ull};
+  SH_ABORT(hip_rc(hipMemcpyAsync(dflag, stat, 16, hipMemcpyHostToDevice, st), "status"));
+  SH_ABORT(T.all_reduce_sum(dflag, 2, st));
+  SH_ABORT(read_back(stat, dflag, 16));
+  if (stat[0]) {
     if (err) return set_error(err, emsg);
-    return set_error(SRS_ERR_OUT_OF_MEMORY, "shard: rank(s) " + rank_list(mask) +
+    return set_error(SRS_ERR_OUT_OF_MEMORY, "shard: rank(s) " + rank_list(stat[1]) +
                                                 " could not allocate before the exchange");
   }
   C->clk.stamp("plan", st);
@@ -894,6 +921,7 @@ int shard_sort(srs_shard_comm C, int64_t n, int kind, int up, const void* keys, 
   // one message group of the schedule, (round, chunk) pieces in order, on
   // the communication stream
   const auto sched = post_schedule(CH, R);
+  int64_t nsend = 0, nrecv = 0;
   auto issue = [&](const std::vector<std::pair<int, int>>& pieces) -> int {
     int rc = T.group_start();
     for (size_t q = 0; q < pieces.size() && rc == SRS_OK; q++)
@@ -901,13 +929,16 @@ int shard_sort(srs_shard_comm C, int64_t n, int kind, int up, const void* keys, 
         if (m.op == 2) continue;
         for (int k = 0; k < ncols && rc == SRS_OK; k++) {
           const size_t wd = width[k];
-          const int64_t per = (int64_t)std::max<size_t>(1, kMsgBytes / wd);
+          const int64_t per = (int64_t)std::max<size_t>(1, cap / wd);
           for (int64_t a = 0; a < m.cnt && rc == SRS_OK; a += per) {
             const size_t bytes = (size_t)std::min(per, m.cnt - a) * wd;
-            if (m.op == 0)
+            if (m.op == 0) {
               rc = T.send((const char*)C->part[k].p + (size_t)(m.src + a) * wd, bytes, m.peer, C->cs);
-            else
+              nsend++;
+            } else {
               rc = T.recv(rcol(k) + (size_t)(m.dst + a) * wd, bytes, m.peer, C->cs);
+              nrecv++;
+            }
           }
         }
       }
@@ -927,6 +958,17 @@ int shard_sort(srs_shard_comm C, int64_t n, int kind, int up, const void* keys, 
 
   // 4. partition chunk by chunk; after chunk c, message group c leaves.
   // A failure from here on is "late": the rank keeps to the message plan.
+  // Until the last status, a workspace buffer that must grow frees its old
+  // memory later (a hipFree now would wait for every receive
+  // already queued, unbounded, and serialise the rounds behind the exchange)
+  struct DeferScope {
+    int64_t* freed;
+    explicit DeferScope(int64_t* f) : freed(f) { defer_workspace_frees(true); }
+    ~DeferScope() {
+      defer_workspace_frees(false);
+      *freed = release_deferred_frees();
+    }
+  } defer_scope(&C->last_deferred);
   int late = 0;
   std::string lmsg;
   auto late_fail = [&](int rc) {
@@ -1012,14 +1054,14 @@ int shard_sort(srs_shard_comm C, int64_t n, int kind, int up, const void* keys, 
   C->clk.stamp("end", st);
 
   // 6. every rank learns whether any rank failed after the first message
-  mask = late ? 1ull << std::min(me, 63) : 0;
-  SH_ABORT(hip_rc(hipMemcpyAsync(dflag, &mask, 8, hipMemcpyHostToDevice, st), "status"));
-  SH_ABORT(T.all_reduce_sum(dflag, 1, st));
-  SH_ABORT(hip_rc(hipMemcpyAsync(&mask, dflag, 8, hipMemcpyDeviceToHost, st), "status"));
-  SH_ABORT(T.wait(st));
-  if (mask) {
+  stat[0] = late ? 1ull : 0ull;
+  stat[1] = late ? 1ull << std::min(me, 63) : 0ull;
+  SH_ABORT(hip_rc(hipMemcpyAsync(dflag, stat, 16, hipMemcpyHostToDevice, st), "status"));
+  SH_ABORT(T.all_reduce_sum(dflag, 2, st));
+  SH_ABORT(read_back(stat, dflag, 16));
+  if (stat[0]) {
     if (late) return set_error(late, lmsg);
-    return set_error(SRS_ERR_INTERNAL, "shard: rank(s) " + rank_list(mask) +
+    return set_error(SRS_ERR_INTERNAL, "shard: rank(s) " + rank_list(stat[1]) +
                                            " failed during the exchange (see their errors)");
   }
   *keys_out = rcol(0);
@@ -1032,6 +1074,10 @@ int shard_sort(srs_shard_comm C, int64_t n, int kind, int up, const void* keys, 
   C->last_out = P.total;
   C->last_rec_bytes = 0;
   for (int k = 0; k < ncols; k++) C->last_rec_bytes += (int)width[k];
+  C->last_self = selfm ? 1 : 0;
+  C->last_cap = (int64_t)cap;
+  C->last_sends = nsend;
+  C->last_recvs = nrecv;
   C->last_sent.clear();
   for (int r = 0; r < R; r++) C->last_sent.push_back(P.sent(r));
   C->last_ok = 1;
@@ -1167,6 +1213,19 @@ int srs_shard_set_options(srs_shard_comm comm, int32_t rounds, int32_t chunks) {
   return SRS_OK;
 }
 
+int srs_shard_set_message_options(srs_shard_comm comm, int32_t self_messages,
+                                  int64_t max_message_bytes) {
+  if (!comm || self_messages < 0 || self_messages > 1 || max_message_bytes < 0 ||
+      max_message_bytes > kMsgBytesMax || max_message_bytes % 64)
+    return set_error(SRS_ERR_INVALID_ARG, "srs_shard_set_message_options: self_messages 0 or 1, "
+                                          "max_message_bytes a multiple of 64 in [0, 2^30] "
+                                          "(0 = 256 MiB)");
+  std::lock_guard<std::mutex> g(comm->mu);
+  comm->self_msgs = self_messages;
+  comm->msg_cap = max_message_bytes;
+  return SRS_OK;
+}
+
 int srs_shard_debug_inject(srs_shard_comm comm, int32_t point) {
   if (!comm || point < 0 || point > 5)
     return set_error(SRS_ERR_INVALID_ARG, "srs_shard_debug_inject: point in [0, 5]");
@@ -1270,7 +1329,12 @@ int srs_shard_last_report(srs_shard_comm comm, char* buf, int64_t cap) {
                   ",\"groups\":" + std::to_string(comm->last_groups) +
                   ",\"records_in\":" + std::to_string(comm->last_in) +
                   ",\"records_out\":" + std::to_string(comm->last_out) +
-                  ",\"record_bytes\":" + std::to_string(comm->last_rec_bytes) + ",\"stamps_ms\":{";
+                  ",\"record_bytes\":" + std::to_string(comm->last_rec_bytes) +
+                  ",\"self_messages\":" + std::to_string(comm->last_self) +
+                  ",\"max_message_bytes\":" + std::to_string(comm->last_cap) +
+                  ",\"sends\":" + std::to_string(comm->last_sends) +
+                  ",\"recvs\":" + std::to_string(comm->last_recvs) +
+                  ",\"deferred_frees\":" + std::to_string(comm->last_deferred) + ",\"stamps_ms\":{";
   const PhaseClock& k = comm->clk;
   for (size_t i = 0; i < k.used; i++) {
     float ms = 0;
@@ -1296,14 +1360,15 @@ int srs_shard_last_report(srs_shard_comm comm, char* buf, int64_t cap) {
 }
 
 int srs_debug_shard_plan(int32_t world, int32_t rank, int32_t chunks, int32_t rounds,
-                         int32_t key_bits, const uint64_t* chunk_hists, int64_t num, char* json,
-                         int64_t cap) {
+                         int32_t key_bits, int32_t self_messages, const uint64_t* chunk_hists,
+                         int64_t num, char* json, int64_t cap) {
   if (world < 1 || rank < 0 || rank >= world || chunks < 1 || chunks > kMaxChunks ||
       rounds < 1 || rounds > kMaxRounds || !chunk_hists || num < 0 || !json ||
+      (self_messages != 0 && self_messages != 1) ||
       (key_bits != 8 && key_bits != 16 && key_bits != 32 && key_bits != 64))
     return set_error(SRS_ERR_INVALID_ARG, "srs_debug_shard_plan: arguments");
   ShardPlan P;
-  P.init(world, rank, chunks, rounds, key_bits);
+  P.init(world, rank, chunks, rounds, key_bits, self_messages != 0);
   const size_t per = (size_t)chunks * P.nb;
   std::vector<uint64_t> tot(P.nb, 0);
   for (int s = 0; s < world; s++)

@@ -41,13 +41,15 @@ def _lib():
         L.srs_shard_comm_init_staged.argtypes = [i32, vp]
         L.srs_shard_comm_destroy.argtypes = [vp]
         L.srs_shard_set_options.argtypes = [vp, i32, i32]
+        L.srs_shard_set_message_options.argtypes = [vp, i32, i64]
         L.srs_shard_debug_inject.argtypes = [vp, i32]
         L.srs_shard_sort_device.argtypes = [vp, i64, ctypes.c_int, ctypes.c_int, vp, i32, vp, vp,
                                             ctypes.POINTER(vp), vp, ctypes.POINTER(i64), vp]
         L.srs_shard_sort_multi.argtypes = [i32, vp, vp, ctypes.c_int, ctypes.c_int, vp, i32, vp,
                                            vp, vp, vp, vp]
         L.srs_shard_last_report.argtypes = [vp, ctypes.c_char_p, i64]
-        L.srs_debug_shard_plan.argtypes = [i32, i32, i32, i32, i32, vp, i64, ctypes.c_char_p, i64]
+        L.srs_debug_shard_plan.argtypes = [i32, i32, i32, i32, i32, i32, vp, i64, ctypes.c_char_p,
+                                           i64]
         _bound = True
     return L
 
@@ -114,6 +116,13 @@ class ShardComm:
         """Exchange rounds and partition chunks (0 = the library default);
         every rank must pass the same."""
         _check(_lib().srs_shard_set_options(self.handle, int(rounds), int(chunks)))
+
+    def set_message_options(self, self_messages: bool = False, max_message_bytes: int = 0) -> None:
+        """Own pieces as messages to this rank instead of device copies, and
+        the largest message (0 = 256 MiB); every rank must pass the same cap
+        (srs_shard_set_message_options)."""
+        _check(_lib().srs_shard_set_message_options(self.handle, int(bool(self_messages)),
+                                                    int(max_message_bytes)))
 
     def inject(self, point: int) -> None:
         """Test hook: the next sort fails at `point` (srs_shard_debug_inject)."""
@@ -208,15 +217,16 @@ def sort_multi(comms, inputs, key_kind: int | None = None, up: bool = True):
 
 
 def debug_plan(world: int, rank: int, chunks: int, rounds: int, key_bits: int, chunk_hists,
-               num: int) -> dict:
+               num: int, self_messages: bool = False) -> dict:
     """srs_debug_shard_plan (host only): the plan rank `rank` follows, from
     every rank's chunk histograms (uint64 numpy array [world][chunks][bins])."""
     import numpy as np
     h = np.ascontiguousarray(chunk_hists, dtype=np.uint64)
     cap = 1 << 26
     buf = ctypes.create_string_buffer(cap)
-    _check(_lib().srs_debug_shard_plan(world, rank, chunks, rounds, key_bits, h.ctypes.data,
-                                       int(num), buf, cap))
+    _check(_lib().srs_debug_shard_plan(world, rank, chunks, rounds, key_bits,
+                                       int(bool(self_messages)), h.ctypes.data, int(num), buf,
+                                       cap))
     return json.loads(buf.value.decode())
 
 

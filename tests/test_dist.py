@@ -71,7 +71,7 @@ def _make_keys(kind, dist_kind, n, rng):
     return np.full(n, 7, dtype=ut)  # all equal
 
 
-def _run_rank(rank, world, kind, dist_kind, n_per, chunks, rounds):
+def _run_rank(rank, world, kind, dist_kind, n_per, chunks, rounds, self_msgs=False):
     shard = _shard()
     rng = np.random.default_rng(100 + rank)
     n = n_per + rank * 17  # ragged shards
@@ -83,7 +83,8 @@ def _run_rank(rank, world, kind, dist_kind, n_per, chunks, rounds):
     allh = [torch.zeros(ch.shape, dtype=torch.int64) for _ in range(world)]
     dist.all_gather(allh, torch.from_numpy(ch.view(np.int64)))
     allh = np.stack([h.numpy().view(np.uint64) for h in allh])
-    plan = shard.debug_plan(world, rank, chunks, rounds, kbits, allh, n)
+    plan = shard.debug_plan(world, rank, chunks, rounds, kbits, allh, n, self_messages=self_msgs)
+    assert not (self_msgs and plan["alias"])
     gob = np.array(plan["group_of_bin"], np.int64)
     # the partition (the device's srs_partition_device): per chunk, stable by group
     top = _top(kind, keys, bits)
@@ -101,12 +102,20 @@ def _run_rank(rank, world, kind, dist_kind, n_per, chunks, rounds):
     else:
         recv_k, recv_p = np.zeros(total, np.int64), np.zeros(total, np.int64)
     cols = [(part_k, recv_k), (part_p, recv_p)]
+    own = []  # self messages in posting order (gloo has no send to self)
     for post in plan["posts"]:
         ops, landings = [], []
         for op, peer, src, dst, cnt in post["msgs"]:
-            assert cnt > 0 and peer != rank or op == 2
+            assert cnt > 0 and (peer != rank or self_msgs) or op == 2
+            assert not (self_msgs and op == 2)
             for sbuf, rbuf in cols:
-                if op == 0:
+                if op == 0 and peer == rank:
+                    own.append(sbuf[src:src + cnt].copy())
+                elif op == 1 and peer == rank:
+                    m = own.pop(0)
+                    assert len(m) == cnt
+                    rbuf[dst:dst + cnt] = m
+                elif op == 0:
                     ops.append(dist.P2POp(dist.isend, torch.from_numpy(sbuf[src:src + cnt].copy()),
                                           peer))
                 elif op == 1:
@@ -141,12 +150,13 @@ def _run_rank(rank, world, kind, dist_kind, n_per, chunks, rounds):
     return keys, pay, rk.view(keys.dtype), recv_p
 
 
-def _worker(rank, world, port, kind, dist_kind, n_per, chunks, rounds, q):
+def _worker(rank, world, port, kind, dist_kind, n_per, chunks, rounds, self_msgs, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        keys, pay, ok, op = _run_rank(rank, world, kind, dist_kind, n_per, chunks, rounds)
+        keys, pay, ok, op = _run_rank(rank, world, kind, dist_kind, n_per, chunks, rounds,
+                                      self_msgs)
         outs = [None] * world
         dist.all_gather_object(outs, (keys, pay, ok, op))
         if rank == 0:
@@ -164,12 +174,12 @@ def _worker(rank, world, port, kind, dist_kind, n_per, chunks, rounds, q):
         dist.destroy_process_group()
 
 
-def _run_world(world, kind, dist_kind, chunks=4, rounds=3, n_per=3000):
+def _run_world(world, kind, dist_kind, chunks=4, rounds=3, n_per=3000, self_msgs=False):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
     procs = [ctx.Process(target=_worker, args=(r, world, port, kind, dist_kind, n_per, chunks,
-                                               rounds, q))
+                                               rounds, self_msgs, q))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -208,10 +218,21 @@ def test_shard_plan_one_rank(chunks, rounds):
     _run_world(1, 6, "uniform", chunks=chunks, rounds=rounds)
 
 
+@pytest.mark.parametrize("world,chunks,rounds", [(1, 1, 4), (1, 8, 16), (3, 4, 8)])
+def test_shard_plan_self_messages(world, chunks, rounds):
+    """srs_shard_set_message_options(self_messages=1): own pieces travel as
+    messages to the rank itself (matched in posting order, as RCCL matches
+    them), never as copies; one chunk at world 1 then no longer aliases the
+    partition buffer. Same result, stable."""
+    _run_world(world, 6, "skewed", chunks=chunks, rounds=rounds, self_msgs=True)
+
+
 # ---- the plan itself, every rank in one process ------------------------------
+@pytest.mark.parametrize("self_msgs", [False, True])
 @pytest.mark.parametrize("world,chunks,rounds,kind", [
-    (2, 8, 8, 6), (3, 4, 16, 6), (8, 8, 8, 6), (8, 16, 64, 6), (5, 2, 3, 0), (4, 8, 8, 2)])
-def test_shard_plan_messages_pair_up(world, chunks, rounds, kind):
+    (2, 8, 8, 6), (3, 4, 16, 6), (8, 8, 8, 6), (8, 16, 64, 6), (5, 2, 3, 0), (4, 8, 8, 2),
+    (1, 8, 16, 6)])
+def test_shard_plan_messages_pair_up(world, chunks, rounds, kind, self_msgs):
     """For every pair of ranks the sends of one match the receives of the
     other in posting order and size; every rank's receives and own copies
     tile its receive buffer exactly once; every partitioned record is sent
@@ -228,7 +249,8 @@ def test_shard_plan_messages_pair_up(world, chunks, rounds, kind):
         for c in range(chunks):
             a, b = _chunk_bound(ns[s], c, chunks), _chunk_bound(ns[s], c + 1, chunks)
             hs[s, c] = np.bincount(top[a:b], minlength=nb)
-    plans = [shard.debug_plan(world, r, chunks, rounds, kbits, hs, ns[r]) for r in range(world)]
+    plans = [shard.debug_plan(world, r, chunks, rounds, kbits, hs, ns[r], self_messages=self_msgs)
+             for r in range(world)]
     assert all(p["group_of_bin"] == plans[0]["group_of_bin"] for p in plans)
     assert all(p["rank_of_group"] == plans[0]["rank_of_group"] for p in plans)
     assert sum(p["total"] for p in plans) == sum(ns)
@@ -239,7 +261,8 @@ def test_shard_plan_messages_pair_up(world, chunks, rounds, kind):
     for i in range(nposts):
         for s in range(world):
             for d in range(world):
-                if s == d:
+                if s == d and not self_msgs:
+                    assert not [m for m in plans[s]["posts"][i]["msgs"] if m[1] == s and m[0] < 2]
                     continue
                 sends = [m[4] for m in plans[s]["posts"][i]["msgs"] if m[0] == 0 and m[1] == d]
                 recvs = [m[4] for m in plans[d]["posts"][i]["msgs"] if m[0] == 1 and m[1] == s]
@@ -255,6 +278,9 @@ def test_shard_plan_messages_pair_up(world, chunks, rounds, kind):
                     used[src:src + cnt] += 1
         if not p["alias"]:
             assert (cover == 1).all() and (used == 1).all(), r
+        if self_msgs:
+            assert not p["alias"]
+            assert not [m for post in p["posts"] for m in post["msgs"] if m[0] == 2]
         rd = p["rounds"]
         assert [x["start"] for x in rd[1:]] == [x["end"] for x in rd[:-1]]
         for x in rd:

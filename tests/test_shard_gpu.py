@@ -167,6 +167,171 @@ def test_shard_rccl_world1_equals_plain_sort(rounds, chunks):
     comm.close()
 
 
+@pytest.mark.parametrize("rounds,chunks,cap", [(16, 8, 64 << 10), (8, 1, 0), (3, 2, 4096)])
+def test_shard_rccl_self_messages(rounds, chunks, cap):
+    """the RCCL point-to-point path on hardware. With self
+    messages a single rank posts every piece as an ncclSend / ncclRecv to
+    itself inside the wavefront's grouped posts (no device copies), with a
+    small message cap forcing the split of each piece into several messages;
+    the receive events on the communication stream and the bounded polling
+    beside in-flight RCCL kernels all run. Equal to the one-GPU sort bit for
+    bit; the report shows the messages and their bytes."""
+    _need_gpu()
+    import srs_amd
+    from srs_amd import shard
+    n = 3_000_017
+    keys = torch.empty(n, dtype=torch.int64, device="cuda")
+    pays = torch.empty(n, dtype=torch.int64, device="cuda")
+    srs_amd.fill_synthetic_device(keys, pays, seed=13 << 32, key_kind=srs_amd.KEY_U64)
+    ko, po = torch.empty_like(keys), torch.empty_like(pays)
+    srs_amd.sort_device(keys, pays, key_kind=srs_amd.KEY_U64, out=(ko, po))
+    comm = shard.ShardComm.rccl(1, 0, shard.unique_id())
+    comm.set_options(rounds, chunks)
+    comm.set_message_options(True, cap)
+    for _ in range(2):  # (buffers reused)
+        k, (p,) = comm.sort(keys, pays, key_kind=srs_amd.KEY_U64)
+        torch.cuda.synchronize()
+        assert torch.equal(k, ko) and torch.equal(p, po)
+    rep = comm.report()
+    assert rep["transport"] == "rccl" and rep["self_messages"] == 1
+    assert rep["max_message_bytes"] == (cap or 256 << 20)
+    pieces = rounds * chunks  # (uniform keys: every (round, chunk) piece is non-empty)
+    assert rep["sends"] == rep["recvs"] >= 2 * pieces
+    if cap and cap < 8 * n // pieces:
+        assert rep["sends"] > 2 * pieces  # (pieces split into several messages)
+    sent = sum(b[0] for b in rep["bytes_to_peer_per_round"])
+    assert sent == 16 * n
+    lf = shard.link_figures(rep)
+    assert lf["busiest_link_bytes"] == 16 * n and lf.get("link_gbs", 0) > 0
+    del k, p
+    comm.close()
+
+
+def test_shard_rccl_self_messages_match_reference():
+    """C1's shape at 2^25 + 1234 records through one rank's RCCL self
+    messages (8 chunks, 16 rounds, 1 MiB messages: each ~2 MB piece of a
+    column split in several): equal to the REFERENCE's own sort
+    (oracle/_ref, radixSort.hpp)."""
+    _need_gpu()
+    import srs_amd
+    from srs_amd import shard
+    from srs_testlib import ref_lib, ref_sort_soa
+    if ref_lib() is None:
+        pytest.fail("oracle/_ref/libsrs_ref.so missing or host lacks AVX-512 VBMI2")
+    n = (1 << 25) + 1234
+    keys = torch.empty(n, dtype=torch.int64, device="cuda")
+    pays = torch.empty(n, dtype=torch.int64, device="cuda")
+    srs_amd.fill_synthetic_device(keys, pays, seed=17 << 32, key_kind=srs_amd.KEY_U64)
+    comm = shard.ShardComm.rccl(1, 0, shard.unique_id())
+    comm.set_options(16, 8)
+    comm.set_message_options(True, 1 << 20)
+    k, (p,) = comm.sort(keys, pays, key_kind=srs_amd.KEY_U64)
+    torch.cuda.synchronize()
+    kr = keys.cpu().numpy().view(np.uint64).copy()
+    pr = pays.cpu().numpy().view(np.uint64).copy()
+    ref_sort_soa(srs_amd.KEY_U64, True, kr, [pr])
+    assert np.array_equal(k.cpu().numpy().view(np.uint64), kr)
+    assert np.array_equal(p.cpu().numpy().view(np.uint64), pr)
+    rep = comm.report()
+    assert rep["sends"] > 2 * 16 * 8 and rep["deferred_frees"] >= 0
+    del k, p
+    comm.close()
+
+
+def test_shard_staged_self_messages():
+    """Self messages over the host-staged transport at world 3 (the FIFO of a
+    rank to itself), with a message cap that splits pieces: the union equals a
+    stable sort."""
+    _need_gpu()
+    from srs_amd import shard
+    comms = shard.staged(3)
+    for c in comms:
+        c.set_options(4, 2)
+        c.set_message_options(True, 8192)
+    inputs = _inputs(3, "skewed", 7, 100_000)
+    outs = shard.sort_multi(comms, inputs, key_kind=7)
+    _check_union(inputs, outs, 7)
+    for r, c in enumerate(comms):
+        rep = c.report()
+        assert rep["self_messages"] == 1
+        assert sum(b[r] for b in rep["bytes_to_peer_per_round"]) > 0
+    del outs
+    for c in comms:
+        c.close()
+
+
+def test_shard_message_cap_must_agree():
+    """Ranks with different message caps would split pieces differently:
+    the header collective fails every rank."""
+    _need_gpu()
+    from srs_amd import shard
+    comms = shard.staged(2)
+    comms[1].set_message_options(False, 4096)
+    inputs = _inputs(2, "uniform", 7, 50_000)
+    with pytest.raises(Exception, match="disagree on the message cap"):
+        shard.sort_multi(comms, inputs, key_kind=7)
+    for c in comms:
+        c.close()
+
+
+def _two_gpus():
+    if not torch.cuda.is_available() or torch.cuda.device_count() < 2:
+        pytest.skip("needs 2 GPUs (RCCL puts no two ranks on one device)")
+
+
+def test_shard_rccl_two_ranks():
+    """two ranks over RCCL (srs_shard_comm_init_all, one thread
+    per rank): the union equals a stable sort of the inputs. Skipped on a
+    one-GPU box (the driver's 8-GPU node runs it)."""
+    _two_gpus()
+    from srs_amd import shard
+    comms = shard.init_all([0, 1])
+    inputs = []
+    for r in range(2):
+        with torch.cuda.device(r):
+            n = 400_000 + 1001 * r
+            g = torch.Generator(device=f"cuda:{r}")
+            g.manual_seed(5 + r)
+            k = torch.randint(-2**63, 2**63 - 1, (n,), dtype=torch.int64, device=f"cuda:{r}",
+                              generator=g)
+            p = torch.arange(n, dtype=torch.int64, device=f"cuda:{r}") + r * 10**7
+            inputs.append((k, [p]))
+    for c in comms:
+        c.set_options(4, 2)
+    outs = shard.sort_multi(comms, inputs, key_kind=7)
+    _check_union(inputs, outs, 7)
+    del outs
+    for c in comms:
+        c.close()
+
+
+@pytest.mark.parametrize("point", [3, 4, 5])
+def test_shard_rccl_two_ranks_failures(point):
+    """failure injection over RCCL at two ranks: a late partition
+    or round-sort failure fails both ranks with the communicators usable; a
+    transport failure aborts both."""
+    _two_gpus()
+    from srs_amd import shard
+    comms = shard.init_all([0, 1])
+    inputs = []
+    for r in range(2):
+        with torch.cuda.device(r):
+            k = torch.randint(-2**63, 2**63 - 1, (200_000,), dtype=torch.int64, device=f"cuda:{r}")
+            inputs.append((k, [torch.arange(200_000, dtype=torch.int64, device=f"cuda:{r}")]))
+    comms[1].inject(point)
+    with pytest.raises(Exception):
+        shard.sort_multi(comms, inputs, key_kind=7)
+    if point == 5:
+        with pytest.raises(Exception, match="aborted"):
+            shard.sort_multi(comms, inputs, key_kind=7)
+    else:
+        outs = shard.sort_multi(comms, inputs, key_kind=7)
+        _check_union(inputs, outs, 7)
+        del outs
+    for c in comms:
+        c.close()
+
+
 def _per_rank_threads(comms, inputs, kind, ranks_opts=None):
     """Each rank's srs_shard_sort_device from its own host thread; returns
     [(ok, error text, seconds)] per rank."""

@@ -1,29 +1,54 @@
 #!/bin/bash
-# Standard GPU session: smoke, GPU tests, benches. Each GPU step has its own
-# time limit; after a crash/abort/timeout (rc >= 124 or rc 134/139) nothing
-# else touches the GPU. A plain test failure (rc 1) does not stop the benches.
+# One parameterised GPU session (replaces the single-use round-5 wrappers):
+#   bash tools/gpu_run.sh <out> step [step ...]
+# Steps (each under its own time limit, output in gpurun_out/<out>/<name>.log):
+#   smoke        __graft_entry__ smoke
+#   tests        the whole -m gpu suite
+#   t:<expr>     -m gpu tests selected by -k <expr>  (e.g. t:shard)
+#   f:<file>     -m gpu tests of tests/<file>.py
+#   exitcheck    the mid-size sorts under rocprofv3 --kernel-trace (the exit-time
+#                crash of VERDICT r05), exit status recorded
+#   b9 / c2 / c3 bench.py at 1e9 (3 steps, no CPU baseline) for C1 / C2 / C3
+#   shard        bench.py --shard (world 1, RCCL, 8 chunks / 16 rounds)
+#   shardself    the same with self messages (own pieces through ncclSend/Recv)
+#   lat          tools/latency.py over the small / mid sizes
+#   bench        the default bench.py line (what the driver runs)
+# After a crash, abort or time limit (rc >= 124, 134, 139) nothing else runs.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-mkdir -p gpurun_out
+OUT=gpurun_out/${1:?usage: gpu_run.sh <out> step...}
+shift
+mkdir -p "$OUT"
+: > "$OUT/steps.txt"
+export TMPDIR=/tmp
+PT="python -u -m pytest -x -q --timeout 240 --timeout-method thread -m gpu"
 step() {  # name timeout cmd...
   local name=$1 to=$2; shift 2
-  timeout -k 10 $to "$@" > gpurun_out/$name.log 2>&1
+  timeout -k 10 "$to" "$@" > "$OUT/$name.log" 2>&1
   local rc=$?
-  echo "$name rc=$rc" >> gpurun_out/steps.txt
-  if [ $rc -ge 124 ] || [ $rc -eq 134 ] || [ $rc -eq 139 ]; then echo "STOP after $name rc=$rc"; exit $rc; fi
+  echo "$name rc=$rc" >> "$OUT/steps.txt"
+  tail -3 "$OUT/$name.log" | sed "s/^/[$name] /"
+  if [ $rc -ge 124 ] || [ $rc -eq 134 ] || [ $rc -eq 139 ]; then
+    echo "STOP after $name rc=$rc"; cat "$OUT/steps.txt"; exit $rc
+  fi
   return 0
 }
-: > gpurun_out/steps.txt
 for s in "$@"; do
   case $s in
     smoke) step smoke 300 python __graft_entry__.py smoke ;;
-    tests) step pytest_gpu 900 python -m pytest tests -m gpu -x -q ;;
-    b8) step bench_1e8 300 python bench.py --n 1e8 --steps 3 --cpu-sample 0 ;;
-    b9) step bench_1e9 600 python bench.py --steps 3 --cpu-sample 0 ;;
-    b9full) step bench_1e9_full 900 python bench.py ;;
-    c2) step bench_c2 600 python bench.py --config c2 --steps 3 --cpu-sample 0 ;;
-    c3) step bench_c3 600 python bench.py --config c3 --steps 3 --cpu-sample 0 ;;
+    tests) step pytest_gpu 900 $PT tests ;;
+    t:*) step "pytest_${s#t:}" 600 $PT tests -k "${s#t:}" ;;
+    f:*) step "pytest_${s#f:}" 600 $PT "tests/${s#f:}.py" ;;
+    exitcheck) step exitcheck 300 rocprofv3 --kernel-trace -d "$OUT/exitcheck_prof" -o run -- \
+                 python tools/latency.py 8192 8193 32768 262144 ;;
+    b9) step bench_c1 600 python bench.py --steps 3 --cpu-sample 0 --extra none ;;
+    c2) step bench_c2 600 python bench.py --config c2 --steps 3 --cpu-sample 0 --extra none ;;
+    c3) step bench_c3 600 python bench.py --config c3 --steps 3 --cpu-sample 0 --extra none ;;
     shard) step bench_shard 600 python bench.py --shard --steps 3 --cpu-sample 0 ;;
-    shardc2) step bench_shard_c2 600 python bench.py --shard --config c2 --steps 3 --cpu-sample 0 ;;
+    shardself) step bench_shard_self 600 python bench.py --shard --self-messages --steps 3 \
+                 --cpu-sample 0 ;;
+    lat) step latency 300 python tools/latency.py ;;
+    bench) step bench_default 900 python bench.py ;;
+    *) echo "unknown step $s"; exit 2 ;;
   esac
 done
-cat gpurun_out/steps.txt
+cat "$OUT/steps.txt"
