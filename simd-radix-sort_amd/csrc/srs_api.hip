@@ -545,8 +545,7 @@ struct Workspace {
   DevBuf prun, ptile, btot, bnt, btile, nt_over, gtile, gorder;
   int64_t gorder_cap = 0;
   DevBuf mid;  // mid-size single launch: the tiles' key OR / AND, their digit counts
-  DevBuf midbar;  // and its grid barriers' arrival words (zeroed once)
-  unsigned long long midbar_base = 0;  // arrivals so far on each of them
+  DevBuf midbar;  // and its grid barrier's words (zeroed once)
   ListCounters* h_ctr = nullptr;
   uint64_t* h_totals = nullptr;
   MidFlag* h_mid = nullptr;        // the mid-size launch's early answer
@@ -1863,7 +1862,8 @@ int run_sort(Workspace* W, const Request& R, hipStream_t st) {
       // sort; buckets over kLocalCap (skewed keys) come back in the big list
       // and continue on the general levels below
       const int64_t T = (n + kTile - 1) / kTile;
-      SRS_TRY(ensure(W->mid, T * 16 + T * kMaxBins * sizeof(uint32_t)));
+      const int64_t part_bytes = mid_part_bytes(n);
+      SRS_TRY(ensure(W->mid, part_bytes + T * kMaxBins * sizeof(uint32_t)));
       if (!W->midbar.p) {
         SRS_TRY(ensure(W->midbar, mid_bar_words() * sizeof(unsigned long long)));
         HIP_TRY(hipMemsetAsync(W->midbar.p, 0, mid_bar_words() * sizeof(unsigned long long), st));
@@ -1880,9 +1880,9 @@ int run_sort(Workspace* W, const Request& R, hipStream_t st) {
         note_elems("mid", (double)n);
         TimedScope ts("mid", (double)0, st);
         e = launch_mid_sort(ksl, d, n, home, (unsigned long long*)W->mid.p,
-                            (uint32_t*)((char*)W->mid.p + T * 16), d_ctr, (Seg*)W->big[0].p,
+                            (uint32_t*)((char*)W->mid.p + part_bytes), d_ctr, (Seg*)W->big[0].p,
                             (unsigned long long*)taken.p, W->h_mid, seq,
-                            (unsigned long long*)W->midbar.p, &W->midbar_base, st);
+                            (unsigned long long*)W->midbar.p, st);
       }
       if (e != hipSuccess) {
         // (a grid the device cannot hold resident: the general path, which

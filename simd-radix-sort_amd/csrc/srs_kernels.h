@@ -80,16 +80,16 @@ void launch_small_sort(int key_size, const SortDesc& d, Seg g, int64_t* taken, h
 // every workgroup resident, else an error and the caller takes the general
 // path); big buckets (> kLocalCap) are appended to `big` with ctr->n_big, and
 // their count reaches the host early through `flag` (MidFlag, host memory).
-// bar: mid_bar_words() u64 of device memory, zeroed once when allocated;
-// *bar_base: the arrivals the earlier launches on it made per word (advanced
-// by this launch's grid size). A call whose barrier timed out posts its seq
-// to flag->err
-constexpr int kMidMaxKeys = 64 * kTile;
+// bar: mid_bar_words() u64 of device memory, zeroed once when allocated and
+// left ready by every launch (a call whose barrier timed out posts its seq
+// to flag->err). part: mid_part_bytes(n); hist: T x kMaxBins u32
+constexpr int kMidMaxKeys = 256 * kTile;
 int mid_bar_words();
+int64_t mid_part_bytes(int64_t n);
 hipError_t launch_mid_sort(int key_size, const SortDesc& d, int64_t n, int src,
                            unsigned long long* part, uint32_t* hist, ListCounters* ctr, Seg* big,
                            unsigned long long* taken, MidFlag* flag, unsigned long long seq,
-                           unsigned long long* bar, unsigned long long* bar_base, hipStream_t st);
+                           unsigned long long* bar, hipStream_t st);
 void launch_local_lsd(int key_size, const SortDesc* d, const Seg* segs,
                       const unsigned long long* nsegs, int grid, hipStream_t st);
 int64_t sample_partial_bytes();

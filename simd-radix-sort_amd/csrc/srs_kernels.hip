@@ -3456,13 +3456,17 @@ __global__ __launch_bounds__(NT) void small_sort_kernel(const SortDesc d, const 
 //      stable, LSD) into OUT; a bucket larger than kLocalCap (skewed keys)
 //      goes to the big list for the host's general levels (ctr->n_big, read
 //      back once).
-// G = max(T tiles, 2^choose_bits(n, 64)) workgroups (<= 128 at kMidMaxKeys):
-// one bucket each, no loop -- a loop over buckets had the compiler hoist the
+// G = max(T tiles, 2^mid_bits(n)) workgroups (<= 256 at kMidMaxKeys): one
+// bucket each, no loop -- a loop over buckets had the compiler hoist the
 // bodies' per-thread invariants out of it and spill 55 VGPRs. One
 // workgroup per CU (129 KB of LDS), so G must fit the chip for the
-// launch (its grid barriers need every workgroup resident).
-constexpr int kMidMaxTiles = 64;  // n <= 262144
-constexpr int kMidMat = 8192;     // tiles x buckets (64 x 128 at kMidMaxKeys)
+// launch (its grid barriers need every workgroup resident). Round 6: up to
+// 2^20 keys (256 tiles, the digit capped at 8 bits: 256 buckets of ~4K);
+// when the T x 2^bits count matrix exceeds the LDS share (kMidMat) the
+// column scans are spread over the grid (phase 2b, one more barrier).
+constexpr int kMidMaxTiles = 256;  // n <= 2^20
+constexpr int kMidMaxBits = 8;     // (G <= 256: every bucket its workgroup)
+constexpr int kMidMat = 8192;      // tiles x buckets scanned in LDS (64 x 128)
 static_assert(kMidMat % kScatterThreads == 0, "count matrix: whole rounds of loads");
 
 struct MidLevelLds {
@@ -3474,37 +3478,45 @@ struct MidLevelLds {
 };
 
 // A grid barrier of the mid-size launch. Every workgroup is resident (the
-// host launches G <= CUs x resident workgroups per CU, one per CU at 129 KB
-// of LDS), so a plain launch with arrival counters replaces the cooperative
-// launch (processes that had made a cooperative launch crashed
-// in the runtime's teardown at exit under rocprofv3). Barrier k counts on its
-// own 64-bit word, which only ever grows: every call passes each of its
-// three barriers once with all G workgroups, so the host knows the count
-// before the call (`base`, the sum of the earlier calls' G) and a barrier is
-// full at base + G; no reset between calls (they are stream-ordered on the
-// workspace). One atomic add per workgroup: a compare-and-swap arrival
-// (tagged words) serialised 128 workgroups' retries, 0.6 ms per call. The
-// agent-scope fences write this workgroup's stores back to the shared point
-// of coherence before it arrives and invalidate stale lines after the wait
-// (workgroups sit on different XCDs, each with its own L2). The wait is
+// host launches G <= CUs x resident workgroups per CU, one per CU at 123 KB
+// of LDS), so a plain launch replaces the cooperative launch (VERDICT r05:
+// processes that had made a cooperative launch crashed in the runtime's
+// teardown at exit under rocprofv3). A central counter with a generation
+// word (sense reversal): each workgroup notes the generation, arrives with
+// one atomic add, and the last to arrive resets the counter and bumps the
+// generation, which releases the others; the words are left ready for the
+// next barrier and the next call (no per-call state in the kernel's
+// arguments: every argument costs SGPRs, and this kernel is at its limit).
+// A compare-and-swap arrival (tagged words) serialised 128 workgroups'
+// retries at 0.6 ms per call. The agent-scope fences write this workgroup's
+// stores back to the shared point of coherence before it arrives (and make
+// the generation read complete first) and invalidate stale lines after the
+// wait (workgroups sit on different XCDs, each with its own L2). The wait is
 // bounded: a barrier that never fills (it cannot, short of a broken
 // residency assumption) posts the call's seq to MidFlag::err and lets the
 // grid drain instead of hanging the GPU; the host checks it.
-constexpr int kMidBarWords = 3;
-__device__ __forceinline__ void mid_grid_barrier(unsigned long long* bar, int k,
-                                                 unsigned long long full, unsigned long long seq,
+constexpr int kMidBarWords = 32;  // u64: the counter and the generation 128 bytes apart
+__device__ __forceinline__ void mid_grid_barrier(unsigned long long* bar, unsigned long long seq,
                                                  MidFlag* flag) {
   __syncthreads();
   if (threadIdx.x == 0) {
-    unsigned long long* w = bar + k;
-    __threadfence();  // (release: this workgroup's global writes)
-    __hip_atomic_fetch_add(w, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    for (uint32_t spin = 0;
-         __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < full; spin++) {
-      __builtin_amdgcn_s_sleep(2);
-      if (spin > (1u << 24)) {  // (seconds: never in a correct run)
-        __hip_atomic_store(&flag->err, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        break;
+    unsigned* cnt = (unsigned*)bar;
+    unsigned* gen = (unsigned*)(bar + 16);
+    const unsigned g0 = __hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __threadfence();  // (release: this workgroup's writes; and g0 is read before arriving)
+    const unsigned old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (old == gridDim.x - 1) {  // the last arrival: reset, then release everyone
+      __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __threadfence();
+      __hip_atomic_fetch_add(gen, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      for (uint32_t spin = 0;
+           __hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == g0; spin++) {
+        __builtin_amdgcn_s_sleep(2);
+        if (spin > (1u << 24)) {  // (seconds: never in a correct run)
+          __hip_atomic_store(&flag->err, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          break;
+        }
       }
     }
     __threadfence();  // (acquire: the other workgroups' writes)
@@ -3527,8 +3539,7 @@ __global__ __launch_bounds__(kLocalThreads) void mid_sort_kernel(
     const SortDesc d, int64_t n, int32_t src, unsigned long long* __restrict__ part,
     uint32_t* __restrict__ hist, ListCounters* __restrict__ ctr, Seg* __restrict__ big,
     unsigned long long* __restrict__ taken, MidFlag* __restrict__ flag, unsigned long long seq,
-    unsigned long long* __restrict__ bar, unsigned long long bar_base) {
-  const unsigned long long full = bar_base + gridDim.x;  // (every barrier of this call)
+    unsigned long long* __restrict__ bar, int wide) {
   static_assert(kLocalThreads == kScatterThreads, "the level phases use the scatter's shape");
   __shared__ MidLds Ls;
   __shared__ int64_t my_start;
@@ -3590,7 +3601,7 @@ __global__ __launch_bounds__(kLocalThreads) void mid_sort_kernel(
     *ctr = ListCounters{};
     taken[0] = taken[1] = 0;
   }
-  mid_grid_barrier(bar, 0, full, seq, flag);
+  mid_grid_barrier(bar, seq, flag);
 
   // ---- 2. the digit; this tile's counts
   // (the T pairs in one round of loads: a loop over them paid a cross-XCD
@@ -3630,14 +3641,10 @@ __global__ __launch_bounds__(kLocalThreads) void mid_sort_kernel(
                         desc->cols[c].stride[BUF_OUT], tbase, ebase, cnt,
                         [&](int k) { return t[k]; });
       }
-    // (uniform over the grid; the later barriers are still passed, so that
-    // every call adds G to each barrier word)
-    mid_grid_barrier(bar, 1, full, seq, flag);
-    mid_grid_barrier(bar, 2, full, seq, flag);
-    return;
+    return;  // (uniform over the grid: no barrier follows)
   }
   const int rbits = 64 - __clzll((long long)var);
-  const int bits = choose_bits(n, rbits);
+  const int bits = min(choose_bits(n, rbits), kMidMaxBits);
   const int shift = rbits - bits;
   const uint32_t nb = 1u << bits, mask = nb - 1;
   if (has_tile) {
@@ -3651,32 +3658,54 @@ __global__ __launch_bounds__(kLocalThreads) void mid_sort_kernel(
     for (uint32_t b = threadIdx.x; b < nb; b += kScatterThreads)
       hist[(size_t)w * kMaxBins + b] = Ls.level.hist[b];
   }
-  mid_grid_barrier(bar, 1, full, seq, flag);
+  mid_grid_barrier(bar, seq, flag);
+  const int TN = T * (int)nb;
+  if (wide) {
+    // ---- 2b. (the count matrix does not fit one workgroup's LDS) workgroup
+    // j < nb scans bucket j's column over the tiles: its tiles' offsets
+    // inside the bucket in place of their counts, the bucket's total in
+    // part[j] (phase 1's words are read: phase 2 is over)
+    const uint32_t i = threadIdx.x;  // (kScatterThreads >= kMidMaxTiles: one tile per thread)
+    if (w < (int)nb) {
+      const uint32_t c = i < (uint32_t)T ? hist[(size_t)i * kMaxBins + w] : 0u;
+      uint32_t all;
+      const uint32_t ex = block_excl_scan<kScatterThreads, uint32_t>(c, Ls.level.sc.scan_sh, &all);
+      if (i < (uint32_t)T) hist[(size_t)i * kMaxBins + w] = ex;
+      if (i == 0) part[w] = all;
+    }
+    mid_grid_barrier(bar, seq, flag);
+  }
 
   // ---- 3. offsets; the stable scatter of the tile into TMP
   {
-    // the T x nb counts into LDS in one round of loads, then summed per bucket
-    const int TN = T * (int)nb;  // (<= kMidMat: the host sizes the launch)
-    uint32_t cv[kMidMat / kScatterThreads];
-#pragma unroll
-    for (int k = 0; k < kMidMat / kScatterThreads; k++) {
-      const int e = (int)threadIdx.x + k * kScatterThreads;
-      cv[k] = e < TN ? hist[(size_t)(e >> bits) * kMaxBins + (e & mask)] : 0u;
-    }
-#pragma unroll
-    for (int k = 0; k < kMidMat / kScatterThreads; k++) {
-      const int e = (int)threadIdx.x + k * kScatterThreads;
-      if (e < TN) Ls.level.mat[e] = cv[k];
-    }
-    __syncthreads();
     const uint32_t b = threadIdx.x;  // (kScatterThreads >= kMaxBins: one bin per thread)
     uint32_t tot = 0, pre = 0;
-    if (b < nb)
-      for (int i = 0; i < T; i++) {
-        const uint32_t c = Ls.level.mat[i * nb + b];
-        tot += c;
-        pre += i < w ? c : 0u;
+    if (wide) {  // (phase 2b's bucket totals and this tile's row of offsets)
+      if (b < nb) {
+        tot = (uint32_t)part[b];
+        pre = has_tile ? hist[(size_t)w * kMaxBins + b] : 0u;
       }
+    } else {
+      // the T x nb counts into LDS in one round of loads, then summed per bucket
+      uint32_t cv[kMidMat / kScatterThreads];
+#pragma unroll
+      for (int k = 0; k < kMidMat / kScatterThreads; k++) {
+        const int e = (int)threadIdx.x + k * kScatterThreads;
+        cv[k] = e < TN ? hist[(size_t)(e >> bits) * kMaxBins + (e & mask)] : 0u;
+      }
+#pragma unroll
+      for (int k = 0; k < kMidMat / kScatterThreads; k++) {
+        const int e = (int)threadIdx.x + k * kScatterThreads;
+        if (e < TN) Ls.level.mat[e] = cv[k];
+      }
+      __syncthreads();
+      if (b < nb)
+        for (int i = 0; i < T; i++) {
+          const uint32_t c = Ls.level.mat[i * nb + b];
+          tot += c;
+          pre += i < w ? c : 0u;
+        }
+    }
     uint32_t all;
     const uint32_t bs = block_excl_scan<kScatterThreads, uint32_t>(tot, Ls.level.sc.scan_sh, &all);
     if (b == (uint32_t)w) {  // (this workgroup's bucket, for phase 4)
@@ -3686,7 +3715,8 @@ __global__ __launch_bounds__(kLocalThreads) void mid_sort_kernel(
     // the host learns now how many buckets come back to it, not at the end
     const int nbig = __syncthreads_count(b < nb && tot > (uint32_t)kLocalCap && shift > 0);
     if (w == 0 && threadIdx.x == 0)
-      mid_tell_host(flag, (unsigned long long)nbig | (nb > (uint32_t)G || TN > kMidMat ? 1ull << 63 : 0), seq);
+      mid_tell_host(flag, (unsigned long long)nbig |
+                              (nb > (uint32_t)G || (!wide && TN > kMidMat) ? 1ull << 63 : 0), seq);
     if (has_tile) {
       if (threadIdx.x == 0) {
         SegPlan& P = Ls.level.plan;
@@ -3713,7 +3743,7 @@ __global__ __launch_bounds__(kLocalThreads) void mid_sort_kernel(
                                                  v1, v2, my_off, DigitLut{});
     }
   }
-  mid_grid_barrier(bar, 2, full, seq, flag);
+  mid_grid_barrier(bar, seq, flag);
 
   // ---- 4. bucket w, into OUT
   const int32_t len = my_len;
@@ -4169,15 +4199,19 @@ void launch_local_lsd(int key_size, const SortDesc* d, const Seg* segs,
 }
 
 int mid_bar_words() { return kMidBarWords; }
+int64_t mid_part_bytes(int64_t n) {  // (part: 2 words per tile, >= 1 word per bucket)
+  return std::max<int64_t>((n + kTile - 1) / kTile, kMidMaxTiles) * 16;
+}
 
 hipError_t launch_mid_sort(int key_size, const SortDesc& d, int64_t n, int src,
                            unsigned long long* part, uint32_t* hist, ListCounters* ctr, Seg* big,
                            unsigned long long* taken, MidFlag* flag, unsigned long long seq,
-                           unsigned long long* bar, unsigned long long* bar_base, hipStream_t st) {
+                           unsigned long long* bar, hipStream_t st) {
   const unsigned T = (unsigned)((n + kTile - 1) / kTile);
-  const unsigned nb_max = 1u << choose_bits(n, 64);
-  if (T > (unsigned)kMidMaxTiles || T * nb_max > (unsigned)kMidMat) return hipErrorInvalidValue;
+  const unsigned nb_max = 1u << std::min(choose_bits(n, 64), kMidMaxBits);
+  if (T > (unsigned)kMidMaxTiles) return hipErrorInvalidValue;
   const unsigned G = std::max(T, nb_max);  // (one bucket per workgroup)
+  const int wide = T * nb_max > (unsigned)kMidMat ? 1 : 0;  // (phase 2b)
   // every workgroup must be resident at once (the grid barriers): G within
   // the device's CUs x the kernel's resident workgroups per CU, else the
   // caller takes the general path (e.g. a partition of a few CUs). Cached
@@ -4204,12 +4238,8 @@ hipError_t launch_mid_sort(int key_size, const SortDesc& d, int64_t n, int src,
   if (resident < 0 || (int64_t)G > (int64_t)resident) return hipErrorCooperativeLaunchTooLarge;
 #define CALL(KT, U, CZ)                                                                         \
   mid_sort_kernel<KT, U, CZ><<<G, kLocalThreads, 0, st>>>(d, n, src, part, hist, ctr, big,    \
-                                                          taken, flag, seq, bar, *bar_base);   \
-  {                                                                                           \
-    const hipError_t le_ = hipGetLastError();                                                 \
-    if (le_ == hipSuccess) *bar_base += G; /* (the launch's arrivals per barrier word) */     \
-    return le_;                                                                               \
-  }
+                                                          taken, flag, seq, bar, wide);       \
+  return hipGetLastError()
   SRS_KEY_DISPATCH(key_size, CALL)
 #undef CALL
   return hipErrorInvalidValue;

@@ -1,6 +1,7 @@
-"""GPU parity tests for the mid-size single launch (kLocalCap < n <= 262144:
-one cooperative launch does the first level and every bucket's local sort,
-DESIGN.md §4 "Mid-size sorts"). The result must equal a stable sort bit for
+"""GPU parity tests for the mid-size single launch (kLocalCap < n <= 2^20:
+one launch with grid barriers does the first level and every bucket's local
+sort, DESIGN.md §6 "Mid-size sorts"; above 2^18 keys with the count
+matrix's column scans spread over the grid). The result must equal a stable sort bit for
 bit in every shape the general path takes at these sizes: separate and in
 place device columns, key + two 4-byte payloads (the general path's pair
 layout is off here), 16-byte records (no slice columns), float keys with
@@ -18,7 +19,7 @@ pytestmark = pytest.mark.gpu
 
 srs_amd = pytest.importorskip("srs_amd")
 
-MID_SIZES = [8193, 12289, 40000, 131072, 262143, 262144]
+MID_SIZES = [8193, 12289, 40000, 131072, 262143, 262144, 262145, 600001, 1048575, 1048576]
 
 
 def _torch():
@@ -115,7 +116,7 @@ def test_mid_all_equal(inplace):
     assert bytes_equal(ok.cpu().numpy(), keys) and bytes_equal(op.cpu().numpy(), pay)
 
 
-@pytest.mark.parametrize("n", [20000, 262144])
+@pytest.mark.parametrize("n", [20000, 262144, 1048576])
 def test_mid_skewed_bucket_continues(n):
     """80 % of the keys share the first digit's bucket (> kLocalCap records):
     that bucket goes back to the host's general levels, the rest are sorted
@@ -251,3 +252,29 @@ def test_many_streams_bound_the_flag_slots():
         assert bytes_equal(dp.cpu().numpy(), idx[order]), i
         stable_n, lsd_n = srs_amd.last_fallbacks()
         assert stable_n >= 0 and lsd_n >= 0
+
+
+@pytest.mark.parametrize("n", [262145, 1 << 20])
+def test_mid_launch_takes_large_sizes(n):
+    """Round 6: 2^18 < n <= 2^20 keys take the one launch (the kernel timing
+    counts one "mid" launch and no count pass), not the general path."""
+    torch = _torch()
+    g = torch.Generator(device="cuda")
+    g.manual_seed(n)
+    keys = torch.randint(-2**63, 2**63 - 1, (n,), dtype=torch.int64, device="cuda", generator=g)
+    pays = torch.arange(n, dtype=torch.int64, device="cuda")
+    ref = stable_reference(7, True, [keys.cpu().numpy(), pays.cpu().numpy()])
+    srs_amd.reset_kernel_stats()
+    srs_amd.set_kernel_timing(True)
+    try:
+        srs_amd.sort_device(keys, pays, key_kind=7)
+        torch.cuda.synchronize()
+    finally:
+        srs_amd.set_kernel_timing(False)
+    def launches(name):
+        try:
+            return srs_amd.kernel_stats(name)[0]
+        except Exception:  # (a family that never ran)
+            return 0
+    assert launches("mid") == 1 and launches("count") == 0
+    assert bytes_equal(keys.cpu().numpy(), ref[0]) and bytes_equal(pays.cpu().numpy(), ref[1])

@@ -16,7 +16,7 @@ import srs_amd  # noqa: E402
 
 def main():
     sizes = [int(float(x)) for x in sys.argv[1:]] or [
-        16, 1024, 4096, 8192, 16384, 32768, 65536, 262144, 1 << 20]
+        16, 1024, 4096, 8192, 16384, 32768, 65536, 262144, 524288, 1 << 20, 1 << 21, 1 << 22]
     dev = torch.device("cuda:0")
     for n in sizes:
         keys = torch.empty(n, dtype=torch.int64, device=dev)
