@@ -519,13 +519,17 @@ inline void cpu_relax() {
 }
 
 int sync_poll(hipStream_t st) {
+  // (spinning for the first 200 us, then yielding the core: the shard's rank
+  // threads, one per GPU, each poll their own read-backs)
   const auto t0 = std::chrono::steady_clock::now();
   for (;;) {
     const hipError_t q = hipStreamQuery(st);
     if (q == hipSuccess) return SRS_OK;
     if (q != hipErrorNotReady) HIP_TRY(q);
-    if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(20)) break;
-    cpu_relax();
+    const auto dt = std::chrono::steady_clock::now() - t0;
+    if (dt > std::chrono::milliseconds(20)) break;
+    if (dt < std::chrono::microseconds(200)) cpu_relax();
+    else std::this_thread::yield();
   }
   HIP_TRY(hipStreamSynchronize(st));
   return SRS_OK;

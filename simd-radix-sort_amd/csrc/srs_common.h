@@ -175,7 +175,10 @@ constexpr int kMaxDigitBits = SRS_MAX_DIGIT_BITS;
 #define SRS_KS_CANON 0x100
 constexpr int kMaxBins = 1 << kMaxDigitBits;   // histogram row stride (tile-major)
 static_assert(kScatterThreads >= kMaxBins, "the scatter tile scan gives one bin per thread");
-constexpr int kScanGroup = 256;                 // tiles per column-scan group
+#ifndef SRS_SCAN_GROUP
+#define SRS_SCAN_GROUP 32
+#endif
+constexpr int kScanGroup = SRS_SCAN_GROUP;      // tiles per column-scan group
 constexpr int kHistMaxBits = 12;                // srs_key_histogram_device
 constexpr int kMaxRanges = 4;                   // key clusters of a range level (lut_mode 2)
 constexpr int kLdsLutBits = 12;                 // flat digit tables up to 4096 entries live in LDS

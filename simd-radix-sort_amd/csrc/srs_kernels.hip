@@ -4237,10 +4237,11 @@ hipError_t launch_mid_sort(int key_size, const SortDesc& d, int64_t n, int src,
   // the device's CUs x the kernel's resident workgroups per CU, else the
   // caller takes the general path (e.g. a partition of a few CUs). Cached
   // per device and key dispatch (the query costs microseconds per call).
-  static std::atomic<int> cap_cache[64][4];  // 0: not queried yet
+  static std::atomic<int> cap_cache[64][6];  // [device][instantiation]; 0: not queried yet
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return hipErrorInvalidValue;
-  const int slot = (key_size & SRS_KS_CANON) ? 3 : (key_size & 0xff) >= 8 ? 2 : (key_size & 0xff) >= 4 ? 1 : 0;
+  const int kb = key_size & 0xff;
+  const int slot = (key_size & SRS_KS_CANON) ? (kb == 4 ? 4 : 5) : kb == 1 ? 0 : kb == 2 ? 1 : kb == 4 ? 2 : 3;
   int resident = cap_cache[dev][slot].load(std::memory_order_relaxed);
   if (resident == 0) {
     int cus = 0, per_cu = 0;

@@ -11,6 +11,8 @@
 #   b9 / c2 / c3 bench.py at 1e9 (3 steps, no CPU baseline) for C1 / C2 / C3
 #   shard        bench.py --shard (world 1, RCCL, 8 chunks / 16 rounds)
 #   shardself    the same with self messages (own pieces through ncclSend/Recv)
+#   shardspan8   the same over keys confined to 1/8 of the key range (one of 8 ranks' span)
+#   profiles     tools/round_profiles.sh $PROFILE_TAG (C1 / C2 / C3 traces + PMC passes)
 #   lat          tools/latency.py over the small / mid sizes
 #   bench        the default bench.py line (what the driver runs)
 # After a crash, abort or time limit (rc >= 124, 134, 139) nothing else runs.
@@ -46,6 +48,9 @@ for s in "$@"; do
     shard) step bench_shard 600 python bench.py --shard --steps 3 --cpu-sample 0 ;;
     shardself) step bench_shard_self 600 python bench.py --shard --self-messages --steps 3 \
                  --cpu-sample 0 ;;
+    shardspan8) step bench_shard_span8 600 python bench.py --shard --dist span8 --steps 3 \
+                 --cpu-sample 0 ;;
+    profiles) step profiles 1500 bash tools/round_profiles.sh "${PROFILE_TAG:-r06}" ;;
     lat) step latency 300 python tools/latency.py ;;
     bench) step bench_default 900 python bench.py ;;
     *) echo "unknown step $s"; exit 2 ;;
