@@ -1143,13 +1143,10 @@ int plan_balanced_level(Workspace* W, const Request& R, const SortDesc& d, bool*
   const int64_t stride = n / blocks;
   // shist: the 64K-bin histogram, then the workgroups' partial rows
   SRS_TRY(ensure(W->shist, 65536 * sizeof(uint32_t) + sample_partial_bytes()));
-  // (AoS records: the key at offset 0 of each record; a whole-range
-  // segment sort whose keys share their top `skip` bits samples the 16 bits
-  // below them)
-  const int skip = R.known_top_bits;
+  // (AoS records: the key at offset 0 of each record)
   if (!launch_sample_hist16(R.in_cols[0], ks, R.aos ? (int)R.elem_size : ks, n, stride,
                             kSampleChunk, blocks, d.mpos, d.mneg,
-                            (uint32_t*)W->shist.p + 65536, (uint32_t*)W->shist.p, st, skip))
+                            (uint32_t*)W->shist.p + 65536, (uint32_t*)W->shist.p, st))
     return fail(SRS_ERR_INTERNAL, "sample histogram: too many keys per workgroup");
   std::vector<uint32_t> h(65536);
   HIP_TRY(hipMemcpyAsync(h.data(), W->shist.p, h.size() * 4, hipMemcpyDeviceToHost, st));
@@ -1162,11 +1159,6 @@ int plan_balanced_level(Workspace* W, const Request& R, const SortDesc& d, bool*
     top9max = std::max(top9max, t);
   }
   if (total == 0) return SRS_OK;
-  if (skip > 0) {  // (known top bits: only the stripe level's spread test; the
-                   // cluster ranges and digit tables work on unshifted bins)
-    *spread = top9max * 512 <= (uint64_t)kBalancedSkew * total;
-    return SRS_OK;
-  }
   // (not with canon_zero: the range level's exact min / max are taken over
   // the raw transformed keys, while its passes map -0.0 onto +0.0's code,
   // which can lie outside them)
@@ -1698,14 +1690,6 @@ bool home_tmp2_enabled() {
   return on;
 }
 
-bool whole_segment_enabled() {  // (SRS_WHOLE_SEGMENT=0: the segment-list path, for A/B)
-  static const bool on = [] {
-    const char* e = getenv("SRS_WHOLE_SEGMENT");
-    return !(e && *e == '0');
-  }();
-  return on;
-}
-
 // medium sorts: both local classes at once (run_sort's local pass)
 constexpr int64_t kLocalForkMaxN = int64_t(1) << 24;
 bool local_fork_enabled() {
@@ -1750,10 +1734,6 @@ int run_sort(Workspace* W, const Request& R, hipStream_t st) {
   const int ks = key_size_of(R.kind);
   const int64_t n = R.num;
   const bool inplace = is_inplace(R);
-  // a whole-range segment sort (srs_sort_segments_device with one segment,
-  // the multi-GPU shard's rounds): every key shares its top `known` bits,
-  // which the first digit skips (and the stripe level can then run)
-  const int known = R.nsegs == 0 ? R.known_top_bits : 0;
 
   // ---- descriptor: key view + columns (AoS records as <= 8-byte slices) --
   SortDesc d;
@@ -1951,7 +1931,7 @@ int run_sort(Workspace* W, const Request& R, hipStream_t st) {
       }
     }
     if (!started) {
-      Seg seg0{0, n, d.key_bits - known, home};
+      Seg seg0{0, n, d.key_bits, home};
       const bool to_local = n <= kLocalCap;
       launch_start(d, d_desc, seg0, to_local ? 1 : 0, (Seg*)W->big[0].p, (Seg*)W->local.p,
                    (Seg*)W->local2.p, d_ctr, st);
@@ -1973,7 +1953,7 @@ int run_sort(Workspace* W, const Request& R, hipStream_t st) {
   // second level's scatter, which writes into one bucket's window, measured
   // 5.9 ms per C1 launch against 7.0 for the first one over the whole array)
   // (a balanced first level: its 512 digit-table groups are the buckets)
-  const int b1 = balanced ? kMaxDigitBits : choose_bits(n, d.key_bits - known);
+  const int b1 = balanced ? kMaxDigitBits : choose_bits(n, d.key_bits);
   const int64_t stripe_len = (int64_t)kStripeKeysPerBucket << b1;
   // Only when the first digit (or the digit table) spreads the keys: a
   // plain level skips a digit all keys share, a stripe level cannot (all-zero
@@ -1986,8 +1966,7 @@ int run_sort(Workspace* W, const Request& R, hipStream_t st) {
     const int64_t K = (n + stripe_len - 1) / stripe_len;
     std::vector<Seg> hs(K);
     for (int64_t k = 0; k < K; k++)
-      hs[k] = Seg{k * stripe_len, std::min(stripe_len, n - k * stripe_len), d.key_bits - known,
-                  home};
+      hs[k] = Seg{k * stripe_len, std::min(stripe_len, n - k * stripe_len), d.key_bits, home};
     SRS_TRY(ensure(W->big[0], K * sizeof(Seg)));
     HIP_TRY(hipMemcpyAsync(W->big[0].p, hs.data(), K * sizeof(Seg), hipMemcpyHostToDevice, st));
     const int nb = 1 << b1;
@@ -2007,7 +1986,7 @@ int run_sort(Workspace* W, const Request& R, hipStream_t st) {
     S.known_len = -1;
     LevelMode m1;
     m1.mode = 1;
-    m1.key_bits = d.key_bits - known;
+    m1.key_bits = d.key_bits;
     ++level;
     if (balanced)
       SRS_TRY(run_level(W, ksl, d_desc, S, kMaxDigitBits, d.lut_mode >= 2 ? 2 : 1, st,
@@ -2878,19 +2857,12 @@ int64_t release_deferred_frees() {
 int reserve_segments_workspace(int64_t num, int ncols, const uint32_t* widths) {
   size_t tmp_bytes = 0;
   for (int c = 0; c < ncols; c++) tmp_bytes += align_up((size_t)std::max<int64_t>(num, 1) * widths[c], 256);
-  // (a whole-range segment sort of a key and two 4-byte payloads moves the
-  // payloads as word pairs through TMP2, run_sort's pair layout)
-  const bool pair = ncols == 3 && widths[1] == 4 && widths[2] == 4;
   Workspace* W = nullptr;
   WsLock lk;
   SRS_TRY(acquire_ws(&W, &lk));
-  const bool tmp_ok = W->tmp.p && W->tmp.bytes >= tmp_bytes;
-  const bool tmp2_ok = !pair || (W->tmp2.p && W->tmp2.bytes >= tmp_bytes);
-  if (tmp_ok && tmp2_ok) return SRS_OK;
-  if (W->idle && W->idle_pending) HIP_TRY(hipEventSynchronize(W->idle));  // (the old buffers' last use)
-  if (!tmp_ok) SRS_TRY(ensure(W->tmp, tmp_bytes, ws_alloc_mode(), true));
-  if (!tmp2_ok) SRS_TRY(ensure(W->tmp2, tmp_bytes, ws_alloc_mode(), true));
-  return SRS_OK;
+  if (W->tmp.p && W->tmp.bytes >= tmp_bytes) return SRS_OK;
+  if (W->idle && W->idle_pending) HIP_TRY(hipEventSynchronize(W->idle));  // (the old TMP's last use)
+  return ensure(W->tmp, tmp_bytes, ws_alloc_mode(), true);
 }
 }  // namespace srs
 
@@ -2983,17 +2955,9 @@ int srs_sort_segments_device(int64_t num, int key_kind, int up, void* keys,
                     nullptr, nullptr));
   SRS_TRY(check_device_alignment(R));
   if (num_segments == 0 || num <= 1) return SRS_OK;
+  R.seg_bounds = segment_bounds;
+  R.nsegs = num_segments;
   R.known_top_bits = known_top_bits;
-  // one segment over the whole range (the shard's rounds) is a whole-array
-  // sort with known top bits: it takes the large-sort levels (stripe first
-  // level, gathered second one) instead of the segment list's plain levels
-  // (round 6: a world-1 shard round of 62.5 M keys 2.3 -> see DESIGN.md §7)
-  const bool whole = num_segments == 1 && segment_bounds[0] == 0 && segment_bounds[1] == num &&
-                     whole_segment_enabled();
-  if (!whole) {
-    R.seg_bounds = segment_bounds;
-    R.nsegs = num_segments;
-  }
   Workspace* W = nullptr;
   WsLock lk;
   SRS_TRY(acquire_ws(&W, &lk));

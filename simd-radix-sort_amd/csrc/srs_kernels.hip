@@ -3815,8 +3815,7 @@ constexpr int kSampleThreads = 1024;
 
 __global__ __launch_bounds__(kSampleThreads) void sample_hist16_kernel(
     const char* __restrict__ keys, int key_bytes, int elem_bytes, int64_t n, int64_t stride,
-    int chunk, int64_t nchunks, uint64_t mpos, uint64_t mneg, uint32_t* __restrict__ partial,
-    int skip) {
+    int chunk, int64_t nchunks, uint64_t mpos, uint64_t mneg, uint32_t* __restrict__ partial) {
   __shared__ uint32_t h2[32768];
   for (uint32_t i = threadIdx.x; i < 32768u; i += kSampleThreads) h2[i] = 0;
   __syncthreads();
@@ -3826,8 +3825,8 @@ __global__ __launch_bounds__(kSampleThreads) void sample_hist16_kernel(
     const int64_t e = min(n, a + chunk);
     for (int64_t i = a + threadIdx.x; i < e; i += kSampleThreads) {
       const uint64_t bits = load_w(keys + i * elem_bytes, key_bytes);  // (AoS: record stride)
-      const uint64_t u = (bits ^ (((bits >> (kb - 1)) & 1) ? mneg : mpos)) << skip;
-      const uint32_t d = (uint32_t)(u >> (kb - 16)) & 0xFFFFu;  // (the 16 bits below `skip`)
+      const uint64_t u = bits ^ (((bits >> (kb - 1)) & 1) ? mneg : mpos);
+      const uint32_t d = (uint32_t)(u >> (kb - 16)) & 0xFFFFu;
       atomicAdd(&h2[d >> 1], 1u << ((d & 1) << 4));
     }
   }
@@ -3929,12 +3928,12 @@ void launch_key_minmax(const void* keys, int key_bytes, int elem_bytes, int64_t 
 
 bool launch_sample_hist16(const void* keys, int key_bytes, int elem_bytes, int64_t n,
                           int64_t stride, int chunk, int64_t blocks, uint64_t mpos, uint64_t mneg,
-                          uint32_t* partial, uint32_t* hist, hipStream_t st, int skip) {
+                          uint32_t* partial, uint32_t* hist, hipStream_t st) {
   const int wgs = (int)std::min<int64_t>(kSampleWGs, std::max<int64_t>(1, blocks));
   // the packed u16 bins of one workgroup must not carry into their neighbour
   if ((blocks + wgs - 1) / wgs * (int64_t)chunk >= 65536) return false;
   sample_hist16_kernel<<<(unsigned)wgs, kSampleThreads, 0, st>>>(
-      (const char*)keys, key_bytes, elem_bytes, n, stride, chunk, blocks, mpos, mneg, partial, skip);
+      (const char*)keys, key_bytes, elem_bytes, n, stride, chunk, blocks, mpos, mneg, partial);
   sample_reduce_kernel<<<32768 / 256, 256, 0, st>>>(partial, wgs, hist);
   return true;
 }

@@ -133,11 +133,11 @@ def _confined(torch, n, kind, top3, seed):
     ((1 << 25) + 1234, "U64", [8], 1), ((1 << 25) + 77, "I64", [8], 6),
     ((1 << 25) + 5, "U32", [4, 4], 2), (3_000_017, "U64", [8], 5), (700_001, "U64", [8], 3)])
 def test_whole_range_segment_known_bits(torch, n, kind, psizes, top3):
-    """Round 6: srs_sort_segments_device with ONE segment over the whole range
-    (the multi-GPU shard's rounds) takes the whole-array levels with the
-    segment's known top bits skipped -- above 2^25 records the stripe first
-    level, below that the general or the mid-size path. Equal to a stable
-    sort bit for bit, with the same result as the segment-list path."""
+    """srs_sort_segments_device with ONE segment over the whole range and
+    known top bits (the multi-GPU shard's rounds), at sizes that take two
+    levels or one: equal to a stable sort bit for bit. (Round 6 measured
+    routing such a segment through the whole-array levels -- stripe first
+    level, known bits skipped: no faster)"""
     k = getattr(srs_amd, "KEY_" + kind)
     keys = _confined(torch, n, k, top3, seed=n + top3)
     g = torch.Generator(device="cuda")
@@ -154,8 +154,7 @@ def test_whole_range_segment_known_bits(torch, n, kind, psizes, top3):
 
 def test_whole_range_segment_skewed_below_known_bits(torch):
     """Known top bits over keys that are also skewed below them (90 % share
-    the next 20 bits): the spread test of the sample (taken below the known
-    bits) keeps the stripe level off, and the result is still exact."""
+    the next 20 bits): exact."""
     n = (1 << 25) + 99
     g = torch.Generator(device="cuda")
     g.manual_seed(3)
