@@ -477,9 +477,9 @@ def measure(cfg_name, args, torch, srs_amd, dist, dev, rank, world, shard):
         rounds, chunks = args.rounds, args.chunks
         if world == 1 and rounds == 0 and chunks == 0:
             # the world-1 line exists to model the 8-GPU run (t8_model): it
-            # runs the plan the library uses at world > 1 (8 chunks, 16
+            # runs the plan the library uses at world > 1 (4 chunks, 8
             # rounds), not world 1's own (one chunk: a 10 ms head)
-            rounds, chunks = 16, 8
+            rounds, chunks = 8, 4
         comm.set_options(rounds, chunks)
         comm.set_message_options(args.self_messages, int(args.msg_cap_mb * (1 << 20)) // 64 * 64)
     shard_out = []

@@ -232,7 +232,7 @@ int srs_shard_comm_destroy(srs_shard_comm comm);
 int srs_shard_comm_init_staged(int32_t world, srs_shard_comm* comms);
 
 /* Exchange rounds (1..64) and partition chunks (1..16) of later sorts on
- * this communicator; 0 = the default (from 2 ranks up 16 rounds and 8
+ * this communicator; 0 = the default (from 2 ranks up 8 rounds and 4
  * chunks; at one rank 8 rounds and 1 chunk). Every rank must use the same values (checked: a mismatch
  * fails every rank with SRS_ERR_INVALID_ARG). */
 int srs_shard_set_options(srs_shard_comm comm, int32_t rounds, int32_t chunks);

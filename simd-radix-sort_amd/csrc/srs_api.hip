@@ -1834,6 +1834,7 @@ int run_sort(Workspace* W, const Request& R, hipStream_t st) {
   ListCounters* d_ctr = (ListCounters*)W->ctr.p;
   int64_t n_big = 0, n_local = 0, n_local2 = 0, n_copy = 0;
   bool mid_continued = false;  // (the big list came from the mid-size launch)
+  int64_t one_seg_len = 0;     // (a segment sort of one large segment: its length)
   if (R.nsegs > 0) {
     // independent segments (multi-GPU receive groups): sorted as sub-ranges
     // of one sort, each starting at the full key width (the varying-bit
@@ -1852,6 +1853,15 @@ int run_sort(Workspace* W, const Request& R, hipStream_t st) {
     SRS_TRY(ensure(W->big[0], std::max<size_t>(1024, hb.size()) * sizeof(Seg)));
     SRS_TRY(ensure(W->local, std::max<size_t>(1024, hl.size()) * sizeof(Seg)));
     SRS_TRY(ensure(W->local2, std::max<size_t>(1024, hl2.size()) * sizeof(Seg)));
+    if (hb.size() == 1 && hl.empty() && hl2.empty()) {
+      // one large segment (the multi-GPU shard's rounds): the lists and the
+      // descriptor in one launch, no host copies and no host wait, and its
+      // first level sized from its length (no totals read-back): ~0.1 ms of
+      // stalls per round sort less
+      launch_start(d, d_desc, hb[0], 0, (Seg*)W->big[0].p, (Seg*)W->local.p, (Seg*)W->local2.p,
+                   d_ctr, st);
+      one_seg_len = hb[0].len;
+    } else {
     if (!hb.empty())
       HIP_TRY(hipMemcpyAsync(W->big[0].p, hb.data(), hb.size() * sizeof(Seg),
                              hipMemcpyHostToDevice, st));
@@ -1870,6 +1880,7 @@ int run_sort(Workspace* W, const Request& R, hipStream_t st) {
     c.local_elems = lel;
     HIP_TRY(hipMemcpyAsync(d_ctr, &c, sizeof c, hipMemcpyHostToDevice, st));
     HIP_TRY(hipStreamSynchronize(st));  // the host vectors go out of scope
+    }
     n_big = (int64_t)hb.size();
     n_local = (int64_t)hl.size();
     n_local2 = (int64_t)hl2.size();
@@ -1946,6 +1957,7 @@ int run_sort(Workspace* W, const Request& R, hipStream_t st) {
   LevelState S{n_big, n_local, n_local2, n_copy, 0, d.ncols, d.tmp2};
   S.pair_tiles = pair_tiles_mode(d, ks, aos_cols);
   if (R.nsegs == 0 && n_big == 1 && !mid_continued) S.known_len = n;
+  if (one_seg_len > 0) S.known_len = one_seg_len;
   int level = 0;
   // Stripe first level: large plain SoA sorts partition
   // stripes of kStripeKeysPerBucket << b1 keys on their own with the first

@@ -146,8 +146,12 @@ constexpr int kHistBins = 1 << kBits;
 constexpr int kGroups = 512;                     // key-range groups
 constexpr int kMaxChunks = 16;                   // partition chunks
 constexpr int kMaxRounds = 64;                   // exchange rounds
-constexpr int kDefaultChunks = 8;                // (world > 1; world 1: one chunk)
-constexpr int kDefaultRounds = 16;               // (world > 1; world 1: 8)
+// (world > 1. Round 6: the world-1 line with the 8-rank plan measured one
+// rank's HBM work at 41.1 ms with 8 rounds / 4 chunks against 44.7 ms with
+// 16 / 8 -- each round sort and each partition chunk costs fixed stalls --
+// while the rounds' tail grows 0.65 -> 1.0 ms)
+constexpr int kDefaultChunks = 4;                // (world 1: one chunk)
+constexpr int kDefaultRounds = 8;                // (world 1: 8)
 constexpr int kDefaultRounds1 = 8;
 constexpr int kHdr = 18;                         // header slots after the histogram
 constexpr size_t kMsgBytes = size_t(256) << 20;  // largest message (default)
