@@ -355,6 +355,9 @@ def main():
         sys.exit(3)
     shard = world > 1 or args.shard
     if shard:
+        # a peer that never arrives ends the library's bounded waits in two
+        # minutes instead of its 10-minute default (a bench step takes < 0.1 s)
+        os.environ.setdefault("SRS_SHARD_TIMEOUT_S", "120")
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29533")
         os.environ.setdefault("RANK", "0")
