@@ -85,3 +85,65 @@ def test_more_gpus_than_visible_fails_loudly():
     assert r.returncode != 0
     assert f"--gpus {n} needs {n} GPUs on this node, {ndev} visible" in r.stderr
     assert '"metric"' not in r.stdout
+
+
+def _verify_worker(rank, world, port, q):
+    import os as _os
+    import sys as _sys
+    import torch
+    import torch.distributed as dist
+    _sys.path.insert(0, REPO)
+    _os.environ["MASTER_ADDR"] = "127.0.0.1"
+    _os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import bench
+        g = torch.Generator()
+        g.manual_seed(5)
+        n = 40_000
+        allk = torch.randint(-2**63, 2**63 - 1, (world * n,), dtype=torch.int64, generator=g)
+        allp = bench._splitmix64(bench._u64_bits(allk, torch), torch)  # payload = f(key)
+        mine = slice(rank * n, (rank + 1) * n)
+        ink, inp = allk[mine].clone(), allp[mine].clone()
+        # the shard contract: rank r holds the r-th key range, sorted (u64 order)
+        order = torch.argsort(allk ^ torch.iinfo(torch.int64).min, stable=True)
+        sk, sp = allk[order], allp[order]
+        cut = [0, world * n // 3, world * n]  # ragged output ranks
+        outk, outp = sk[cut[rank]:cut[rank + 1]], sp[cut[rank]:cut[rank + 1]]
+        good = bench.verify_shards(ink, [inp], (outk, [outp]), "u64", [8], torch, dist, "cpu")
+        # a broken output: rank 1 drops its last record and repeats its first
+        if rank == 1:
+            outk = torch.cat([outk[:1], outk[:-1]])
+            outp = torch.cat([outp[:1], outp[:-1]])
+        bad = bench.verify_shards(ink, [inp], (outk, [outp]), "u64", [8], torch, dist, "cpu")
+        if rank == 0:
+            q.put(("ok", good, bad))
+    except Exception as e:  # report instead of hanging the parent
+        q.put(("error", repr(e), None))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+def test_verify_shards_over_gloo():
+    """The N > 1 bench line's full-size check (bench.verify_shards: every rank
+    sorted with payload = f(key), rank boundaries ordered, the multiset hash
+    and count over all ranks unchanged) on two gloo ranks: a correct shard
+    output passes every check, a rank that lost a record fails the hash."""
+    import socket
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_verify_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = q.get(timeout=180)
+    for p in ps:
+        p.join(timeout=60)
+    assert res[0] == "ok", res
+    good, bad = res[1], res[2]
+    assert all(good.values()), good
+    assert not bad["multiset_hash_equal"], bad
