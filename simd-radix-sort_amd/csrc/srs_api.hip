@@ -2259,7 +2259,12 @@ int sort_device(Request& R, hipStream_t st) {
 constexpr int kStageThreads = 4;
 constexpr int kStageBufs = 3;
 constexpr size_t kStageChunk = size_t(32) << 20;
-constexpr size_t kStageMinBytesDefault = size_t(16) << 20;  // below: one pageable hipMemcpy
+// below: one pageable hipMemcpy per column. Round 6 (tools/host_latency.py,
+// host_rate.py; profiles/r06/host/): with ROCm 7.2 the runtime's own pageable
+// copy reaches 1.06-1.12x the PCIe bound for columns of 16 MB to 2 GB, where
+// the staging rings managed 1.25-2.2x; at 8 GB columns (1e9 records) the
+// rings stay ahead (1.07-1.10x against 1.13x). (round 5: 16 MB)
+constexpr size_t kStageMinBytesDefault = size_t(4) << 30;
 constexpr size_t kPackedMaxBytes = size_t(256) << 10;       // below: all columns in one DMA
 constexpr size_t kZeroCopyMaxBytes = size_t(2) << 20;       // below: kernels on host memory
 size_t stage_min_bytes() {  // (SRS_STAGE_MIN_MB overrides, for experiments)
