@@ -126,10 +126,11 @@ int srs_sort_aos_leaf(int64_t num, int key_kind, int up, int64_t cmp_sort_thresh
  * *_out arrays (which must not alias the inputs). The call enqueues work and
  * may block briefly on small control read-backs; results are ready when the
  * stream completes. By size: num <= 8192 is one launch and no host wait;
- * 8192 < num <= 262144 (no segment list) is one cooperative launch, and the
- * call waits until that kernel has posted its first level's bucket sizes to
- * host memory (a skewed input then continues on the general levels); larger
- * sorts read back a small counter block once per global level. */
+ * 8192 < num <= 2^20 (no segment list) is one launch with its own grid
+ * barriers, and the call waits until that kernel has posted its first
+ * level's bucket sizes to host memory (a skewed input then continues on the
+ * general levels); larger sorts read back a small counter block once per
+ * global level. */
 int srs_sort_soa_device(int64_t num, int key_kind, int up,
                         int64_t cmp_sort_threshold, void* keys,
                         int32_t num_payloads, void* const* payloads,

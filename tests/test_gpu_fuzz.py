@@ -1,9 +1,9 @@
 """Randomised parity sweep over the entry points and the size classes the
-round-5 paths split on (single-workgroup small sorts on 128-1024 threads,
-the mid-size cooperative launch, the general levels; host arrays through
+round-5/6 paths split on (single-workgroup small sorts on 128-1024 threads,
+the mid-size single launch up to 2^20 keys, the general levels; host arrays through
 coherent pinned memory, the packed DMA or the staged copies; device arrays
 in place or out of place): 600 seeded cases of random key kind, direction,
-size (log-uniform 1 .. 300000), key distribution and payload columns, each
+size (log-uniform 1 .. 1.2M), key distribution and payload columns, each
 equal to a stable sort bit for bit (the GPU sort is stable; with n <=
 cmp_sort_threshold floats compare -0.0 == +0.0, as the reference's leaf).
 NaN keys are outside the contract and not generated."""
@@ -68,7 +68,7 @@ def test_fuzz_case(case):
     rng = np.random.default_rng(1_000_003 * case + 17)
     kind = int(rng.integers(0, 10))
     up = bool(rng.integers(0, 2))
-    n = int(np.exp(rng.uniform(0, np.log(300_000))))
+    n = int(np.exp(rng.uniform(0, np.log(1_200_000))))
     dist = ["full", "narrow", "const", "skew"][int(rng.integers(0, 4))]
     keys = _keys(kind, n, dist, rng)
     widths = [int(w) for w in rng.choice([1, 2, 4, 8], int(rng.integers(0, 3)))]
