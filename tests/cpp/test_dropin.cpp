@@ -296,9 +296,16 @@ int main(int argc, char** argv) {
   }
   for (std::size_t n = 1; n <= max_num; n *= 10) {
     const long before = g_failed;
+    // (a progress line per quarter: at n = 1e6 a quarter takes about a minute)
     all_types<false, true>(n, seed);
+    std::printf("  n=%zu: separate, up done\n", n);
+    std::fflush(stdout);
     all_types<false, false>(n, seed);
+    std::printf("  n=%zu: separate, down done\n", n);
+    std::fflush(stdout);
     all_types<true, true>(n, seed);
+    std::printf("  n=%zu: combined, up done\n", n);
+    std::fflush(stdout);
     all_types<true, false>(n, seed);
     std::printf("Testing %zu elements: %s\n", n, g_failed == before ? "passed" : "FAILED");
     std::fflush(stdout);
