@@ -1708,6 +1708,17 @@ bool mid_enabled() {
   return on;
 }
 
+// the largest sort whose first level takes one launch (launch_mid_level);
+// SRS_MID_LEVEL_MAX (records, <= kMidLevelMaxKeys) for A/B runs, 0 off
+int64_t mid_level_max_n() {
+  static const int64_t v = [] {
+    const char* e = getenv("SRS_MID_LEVEL_MAX");
+    const int64_t x = e && *e ? (int64_t)atof(e) : kMidLevelMaxKeys;
+    return std::min<int64_t>(x, kMidLevelMaxKeys);
+  }();
+  return v;
+}
+
 // Waits for the mid-size kernel's MidFlag of call `seq`: a short poll, then
 // the stream (which also surfaces a kernel failure).
 int wait_mid_flag(const MidFlag* f, unsigned long long seq, hipStream_t st) {
@@ -1745,6 +1756,9 @@ int run_sort(Workspace* W, const Request& R, hipStream_t st) {
   const int ksl = ks | (d.canon_zero ? SRS_KS_CANON : 0);  // kernel dispatch key
   // (the mid-size launch moves the columns as they are: no slices, no pairs)
   const bool mid = R.nsegs == 0 && n > kLocalCap && n <= kMidMaxKeys && mid_enabled();
+  // (above it, the first level in one launch; the layout is the general path's
+  // except C2's interleaved pair words, which that launch's scatter does not write)
+  const bool mid1 = R.nsegs == 0 && n > kMidMaxKeys && n <= mid_level_max_n() && mid_enabled();
 
   // AoS records of 16+ bytes travel as SoA slice columns through the
   // workspace (TMP, TMP2) between the first scatter and the local pass: the
@@ -1757,7 +1771,7 @@ int run_sort(Workspace* W, const Request& R, hipStream_t st) {
   // 32-byte runs (the same bytes as one 8-byte payload column measured
   // 23.6 -> 21.1 ms at 1e9)
   const bool pair_cols = !R.aos && R.ncols == 3 && R.widths[1] == 4 && R.widths[2] == 4 &&
-                         n > kLocalCap && R.nsegs == 0 && !mid;
+                         n > kLocalCap && R.nsegs == 0 && !mid && !mid1;
   // Home write (round 6): when the output columns are not placement-probed
   // memory (srs_alloc_device) -- the reference's in-place contract
   // (radixSort.hpp:1780) on the caller's own array, or any array of the
@@ -1767,7 +1781,8 @@ int run_sort(Workspace* W, const Request& R, hipStream_t st) {
   // what an unlucky placement slows down (6.2 vs 7.0 ms per
   // launch); a streaming write is far less exposed. (SRS_HOME_TMP2=0: off)
   bool home_tmp2 = false;
-  if (!R.aos && !pair_cols && n >= kHomeTmp2MinN && R.nsegs == 0 && !mid && home_tmp2_enabled()) {
+  if (!R.aos && !pair_cols && n >= kHomeTmp2MinN && R.nsegs == 0 && !mid && !mid1 &&
+      home_tmp2_enabled()) {
     for (int c = 0; c < R.ncols && !home_tmp2; c++)
       home_tmp2 = !placed_memory(R.out_cols[c], (size_t)n * R.widths[c]);
   }
@@ -1938,6 +1953,49 @@ int run_sort(Workspace* W, const Request& R, hipStream_t st) {
         }
         launch_set_desc(d, d_desc, st);
         W->h_ctr->local_elems = 0;
+        started = true;
+      }
+    }
+    if (mid1) {
+      // the first level in one launch (grid barriers); the work lists and
+      // their lengths come back as after a general first level
+      const int64_t T = (n + kTile - 1) / kTile;
+      const int64_t part_bytes = mid_level_part_bytes();
+      SRS_TRY(ensure(W->mid, part_bytes + T * kMaxBins * sizeof(uint32_t)));
+      if (!W->midbar.p) {
+        SRS_TRY(ensure(W->midbar, mid_bar_words() * sizeof(unsigned long long)));
+        HIP_TRY(hipMemsetAsync(W->midbar.p, 0, mid_bar_words() * sizeof(unsigned long long), st));
+      }
+      auto barrier_failed = [&] { return __atomic_load_n(&W->h_mid->err, __ATOMIC_ACQUIRE) != 0; };
+      if (barrier_failed())
+        return fail(SRS_ERR_INTERNAL, "mid-size launch: a grid barrier timed out");
+      hipError_t e;
+      const unsigned long long seq = ++W->mid_seq;
+      {
+        note_elems("mid_level", (double)n);
+        TimedScope ts("mid_level", (double)0, st);
+        e = launch_mid_level(ksl, d, n, home, (unsigned long long*)W->mid.p,
+                             (uint32_t*)((char*)W->mid.p + part_bytes), d_ctr, (Seg*)W->big[0].p,
+                             (Seg*)W->local.p, (Seg*)W->local2.p, (Seg*)W->copy.p, d_desc,
+                             W->h_mid, seq, (unsigned long long*)W->midbar.p, st);
+      }
+      if (e != hipSuccess) {
+        (void)hipGetLastError();
+        if (trace_levels())
+          fprintf(stderr, "[srs] mid-level launch refused (%s): general path\n", hipGetErrorString(e));
+      } else {
+        SRS_TRY(wait_mid_flag(W->h_mid, seq, st));
+        if (barrier_failed())
+          return fail(SRS_ERR_INTERNAL, "mid-size launch: a grid barrier timed out");
+        n_big = (int64_t)__atomic_load_n(&W->h_mid->n_big, __ATOMIC_ACQUIRE);
+        n_local = (int64_t)__atomic_load_n(&W->h_mid->n_local, __ATOMIC_ACQUIRE);
+        n_local2 = (int64_t)__atomic_load_n(&W->h_mid->n_local2, __ATOMIC_ACQUIRE);
+        n_copy = (int64_t)__atomic_load_n(&W->h_mid->n_copy, __ATOMIC_ACQUIRE);
+        W->h_ctr->local_elems = __atomic_load_n(&W->h_mid->local_elems, __ATOMIC_ACQUIRE);
+        if (trace_levels())
+          fprintf(stderr, "[srs] mid-level: big %lld, local %lld, local2 %lld, copy %lld\n",
+                  (long long)n_big, (long long)n_local, (long long)n_local2, (long long)n_copy);
+        if (n_big + n_local + n_local2 + n_copy == 0) return SRS_OK;  // (keys all equal: copied)
         started = true;
       }
     }

@@ -124,6 +124,8 @@ struct MidFlag {
   unsigned long long n_big;  // buckets handed back to the general levels (bit 63: error)
   unsigned long long seq;    // the call's sequence number
   unsigned long long err;    // the seq of a call whose grid barrier timed out (0: none)
+  // (mid_level_kernel) the other lists' lengths and the local lists' records
+  unsigned long long n_local, n_local2, n_copy, local_elems;
 };
 
 // Work-list counters (device), read back by the host once per level.

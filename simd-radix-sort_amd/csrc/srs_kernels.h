@@ -90,6 +90,20 @@ hipError_t launch_mid_sort(int key_size, const SortDesc& d, int64_t n, int src,
                            unsigned long long* part, uint32_t* hist, ListCounters* ctr, Seg* big,
                            unsigned long long* taken, MidFlag* flag, unsigned long long seq,
                            unsigned long long* bar, hipStream_t st);
+// kMidMaxKeys < n <= kMidLevelMaxKeys: the FIRST level in one launch
+// (mid_level_kernel: count, column scans and scatter into TMP with grid
+// barriers, the workgroups looping over tiles). The buckets go to the work
+// lists as a level's would; their lengths reach the host through `flag`
+// before the scatter ends (MidFlag n_big / n_local / n_local2 / n_copy), so
+// the caller enqueues the LDS pass without a read-back. Writes the
+// descriptor to d_out and resets ctr. part: mid_level_part_bytes(); hist: T x
+// kMaxBins u32. Every workgroup resident, else an error (the general path).
+constexpr int kMidLevelMaxKeys = 1024 * kTile;
+int64_t mid_level_part_bytes();
+hipError_t launch_mid_level(int key_size, const SortDesc& d, int64_t n, int src,
+                            unsigned long long* part, uint32_t* hist, ListCounters* ctr, Seg* big,
+                            Seg* local, Seg* local2, Seg* copy, SortDesc* d_out, MidFlag* flag,
+                            unsigned long long seq, unsigned long long* bar, hipStream_t st);
 void launch_local_lsd(int key_size, const SortDesc* d, const Seg* segs,
                       const unsigned long long* nsegs, int grid, hipStream_t st);
 int64_t sample_partial_bytes();

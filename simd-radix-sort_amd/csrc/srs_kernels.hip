@@ -3805,6 +3805,288 @@ __global__ __launch_bounds__(kLocalThreads) void mid_sort_kernel(
 }
 
 // ---------------------------------------------------------------------------
+// the first level of a kMidMaxKeys < n <= kMidLevelMaxKeys sort in ONE launch
+// ---------------------------------------------------------------------------
+// Past the mid-size launch (one bucket per resident workgroup) the general
+// path's first level costs a start kernel, a plan, a tile map, the count,
+// three scan kernels, the scatter and a list read-back before the LDS pass
+// can be enqueued: ~60 us of launch gaps and host wait around ~15 us of
+// memory work at 2^21 keys. Here one launch of G = min(T, resident)
+// workgroups, each looping over tiles w, w + G, ..., does it with two grid
+// barriers (mid_grid_barrier, light: only count words cross them):
+//   A. every tile's digit counts at the full key width (a level's digit:
+//      choose_bits), and each workgroup's key OR / AND;
+//   -- barrier; the keys' varying bits: when the digit lies above them
+//      (every key in one bucket) A runs again below them (uniform decision,
+//      at most once: the recount's digit holds the top varying bit);
+//   B. workgroup j scans bucket j's column over the tiles (<= 1024: one per
+//      thread), the tiles' offsets in place, the bucket's total;
+//   -- barrier;
+//   C. bucket bases (one scan per workgroup); workgroup 0 appends the
+//      buckets to the work lists with a level's classes (emit_child) and
+//      posts the lists' lengths to the host (MidFlag) -- the host enqueues the
+//      LDS pass while the scatter runs; every tile is scattered into TMP with
+//      the global levels' code (scatter_process_tile).
+// The host continues exactly as after a general first level (skewed keys:
+// big buckets take the general levels). Keys equal throughout: copied to OUT.
+constexpr int kMidLevelMaxTiles = kMidLevelMaxKeys / kTile;
+static_assert(kMidLevelMaxTiles <= kScatterThreads, "column scans: one tile per thread");
+static_assert(kMaxBins <= kScatterThreads, "bucket scan: one bucket per thread");
+
+__device__ __forceinline__ void copy_desc(const SortDesc& d, SortDesc* out);
+
+struct MidLevel1Lds {
+  ScatterLds<0> sc;
+  SegPlan plan;
+  unsigned long long wor[kScatterThreads / 64], wand[kScatterThreads / 64];
+  uint32_t hist[kMaxBins];
+  uint32_t cls[5];  // list lengths (big, local, local2, copy) and the local lists' records
+};
+
+template <typename KT, typename U, bool CZ>
+__global__ __launch_bounds__(kScatterThreads) void mid_level_kernel(
+    const SortDesc d, int64_t n, int32_t src, unsigned long long* __restrict__ part,
+    uint32_t* __restrict__ hist, ListCounters* __restrict__ ctr, Seg* __restrict__ big,
+    Seg* __restrict__ local, Seg* __restrict__ local2, Seg* __restrict__ copy,
+    SortDesc* __restrict__ d_out, MidFlag* __restrict__ flag, unsigned long long seq,
+    unsigned long long* __restrict__ bar) {
+  __shared__ MidLevel1Lds L;
+  const SortDesc* desc = &d;
+  constexpr int IT = kScatterItems;
+  constexpr int NT = kScatterThreads;
+  const int G = (int)gridDim.x;
+  const int T = (int)((n + kTile - 1) / kTile);
+  const int w = (int)blockIdx.x;
+  const uint32_t wave = threadIdx.x >> 6, lane = lane_id();
+  const int ebase = (int)wave * IT * 64 + (int)lane;
+  const int ncols = desc->ncols;
+  Xform<U, CZ> xf;
+  xf.init(*desc);
+  const int kbytes = desc->key_bits >> 3;
+  const uint64_t kmask = kbytes == 8 ? ~0ull : ((1ull << (8 * kbytes)) - 1);
+  auto tile_cnt = [&](int t) { return (int)std::min<int64_t>(kTile, n - (int64_t)t * kTile); };
+  unsigned long long* tot_w = part;             // [kMaxBins] bucket totals (B)
+  unsigned long long* var_w = part + kMaxBins;  // [2 G] the workgroups' key OR / AND (A)
+  if (w == 0) {
+    copy_desc(d, d_out);  // (for the kernels that follow)
+    if (threadIdx.x == 0) *ctr = ListCounters{};
+  }
+
+  int rbits = desc->key_bits, bits = 0, shift = 0;
+  uint32_t nb = 0;
+  for (int pass = 0;; pass++) {
+    bits = min(choose_bits(n, rbits), kMaxDigitBits);
+    shift = rbits - bits;
+    nb = 1u << bits;
+    const uint32_t mask = nb - 1;
+    // ---- A. the tiles' digit counts; the keys' OR / AND
+    unsigned long long kor = 0, kand = ~0ull;
+    // (the next tile's keys are loaded while this one is counted)
+    uint64_t nv[IT];
+    if (w < T)
+      load_strip<IT>(nv, desc->cols[0].base[src], desc->cols[0].width, desc->cols[0].stride[src],
+                     (int64_t)w * kTile, ebase, tile_cnt(w));
+    for (int t = w; t < T; t += G) {
+      const int cnt = tile_cnt(t);
+      uint64_t v[IT];
+#pragma unroll
+      for (int k = 0; k < IT; k++) v[k] = nv[k];
+      if (t + G < T)
+        load_strip<IT>(nv, desc->cols[0].base[src], desc->cols[0].width,
+                       desc->cols[0].stride[src], (int64_t)(t + G) * kTile, ebase, tile_cnt(t + G));
+      __syncthreads();  // (the previous tile's row has been read out)
+      if (threadIdx.x < (uint32_t)kMaxBins) L.hist[threadIdx.x] = 0;
+      __syncthreads();
+#pragma unroll
+      for (int k = 0; k < IT; k++)
+        if (ebase + k * 64 < cnt) {
+          const unsigned long long u = (unsigned long long)xf((U)(v[k] & kmask));
+          kor |= u;
+          kand &= u;
+          atomicAdd(&L.hist[(uint32_t)(u >> shift) & mask], 1u);
+        }
+      __syncthreads();
+      if (threadIdx.x < nb) mid_st(&hist[(size_t)t * kMaxBins + threadIdx.x], L.hist[threadIdx.x]);
+    }
+    if (pass == 0) {
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        kor |= __shfl_xor(kor, o, 64);
+        kand &= __shfl_xor(kand, o, 64);
+      }
+      if (lane == 0) {
+        L.wor[wave] = kor;
+        L.wand[wave] = kand;
+      }
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        unsigned long long o = 0, a = ~0ull;
+        for (int i = 0; i < NT / 64; i++) {
+          o |= L.wor[i];
+          a &= L.wand[i];
+        }
+        mid_st(&var_w[2 * w], o);
+        mid_st(&var_w[2 * w + 1], a);
+      }
+    }
+    mid_grid_barrier<false>(bar, seq, flag);
+    if (pass == 0) {
+      // the varying bits (G <= NT pairs: one round of loads)
+      unsigned long long o = 0, a = ~0ull;
+      if (threadIdx.x < (uint32_t)G) {
+        o = mid_ld(&var_w[2 * threadIdx.x]);
+        a = mid_ld(&var_w[2 * threadIdx.x + 1]);
+      }
+#pragma unroll
+      for (int s = 32; s > 0; s >>= 1) {
+        o |= __shfl_xor(o, s, 64);
+        a &= __shfl_xor(a, s, 64);
+      }
+      __syncthreads();  // (the reads of wor / wand above are over)
+      if (lane == 0) {
+        L.wor[wave] = o;
+        L.wand[wave] = a;
+      }
+      __syncthreads();
+      unsigned long long gor = 0, gand = ~0ull;
+      for (int i = 0; i < NT / 64; i++) {
+        gor |= L.wor[i];
+        gand &= L.wand[i];
+      }
+      const unsigned long long var = gor ^ gand;
+      if (var == 0) {  // every key equal: the input is the output (stable)
+        if (w == 0) {
+          __syncthreads();  // (copy_desc above; nothing follows on the device)
+          if (threadIdx.x == 0) {
+            __hip_atomic_store(&flag->n_local, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(&flag->n_local2, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(&flag->n_copy, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            mid_tell_host(flag, 0, seq);
+          }
+        }
+        if (src != BUF_OUT)
+          for (int t = w; t < T; t += G) {
+            const int cnt = tile_cnt(t);
+            for (int c = 0; c < ncols; c++) {
+              uint64_t tv[IT];
+              load_strip<IT>(tv, desc->cols[c].base[src], desc->cols[c].width,
+                             desc->cols[c].stride[src], (int64_t)t * kTile, ebase, cnt);
+              store_strip<IT>(desc->cols[c].base[BUF_OUT], desc->cols[c].width,
+                              desc->cols[c].stride[BUF_OUT], (int64_t)t * kTile, ebase, cnt,
+                              [&](int k) { return tv[k]; });
+            }
+          }
+        return;  // (uniform over the grid: no barrier follows)
+      }
+      const int vb = 64 - __clzll((long long)var);
+      if (vb <= shift) {  // (every key in one bucket: count again below the shared bits)
+        rbits = vb;
+        continue;
+      }
+    }
+    // ---- B. bucket j's column: the tiles' offsets inside it, its total
+    for (uint32_t j = (uint32_t)w; j < nb; j += (uint32_t)G) {
+      const uint32_t i = threadIdx.x;
+      const uint32_t c = i < (uint32_t)T ? mid_ld(&hist[(size_t)i * kMaxBins + j]) : 0u;
+      uint32_t all;
+      const uint32_t ex = block_excl_scan<NT, uint32_t>(c, L.sc.scan_sh, &all);
+      if (i < (uint32_t)T) mid_st(&hist[(size_t)i * kMaxBins + j], ex);
+      if (i == 0) mid_st(&tot_w[j], (unsigned long long)all);
+      __syncthreads();  // (scan_sh is reused)
+    }
+    mid_grid_barrier<false>(bar, seq, flag);
+    break;
+  }
+
+  // ---- C. bucket bases; the work lists; the scatter into TMP
+  const uint32_t b = threadIdx.x;
+  const uint32_t tot = b < nb ? (uint32_t)mid_ld(&tot_w[b]) : 0u;
+  uint32_t all;
+  const uint32_t bs = block_excl_scan<NT, uint32_t>(tot, L.sc.scan_sh, &all);
+  if (w == 0) {
+    // a level's classes (emit_child): final buckets (no bits left, or one
+    // record) are copied by the LDS pass or, past its capacity, the copy list
+    int cls = -1;
+    if (tot > 0) {
+      const bool fin = shift == 0 || tot == 1;
+      cls = tot <= (uint32_t)kLocalCapSmall ? 1 : tot <= (uint32_t)kLocalCap ? 2 : fin ? 3 : 0;
+    }
+    if (threadIdx.x < 5) L.cls[threadIdx.x] = 0;
+    __syncthreads();
+    uint32_t my = 0;
+    if (cls >= 0) my = atomicAdd(&L.cls[cls], 1u);
+    if (cls == 1 || cls == 2) atomicAdd(&L.cls[4], tot);
+    __syncthreads();
+    if (cls >= 0) {
+      Seg* list = cls == 0 ? big : cls == 1 ? local : cls == 2 ? local2 : copy;
+      list[my] = Seg{(int64_t)bs, (int64_t)tot, shift, BUF_TMP};
+    }
+    if (threadIdx.x == 0) {
+      ctr->n_big = L.cls[0];
+      ctr->n_local = L.cls[1];
+      ctr->n_local2 = L.cls[2];
+      ctr->n_copy = L.cls[3];
+      ctr->local_elems = L.cls[4];
+      __hip_atomic_store(&flag->n_local, (unsigned long long)L.cls[1], __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(&flag->n_local2, (unsigned long long)L.cls[2], __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(&flag->n_copy, (unsigned long long)L.cls[3], __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(&flag->local_elems, (unsigned long long)L.cls[4], __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
+      mid_tell_host(flag, L.cls[0], seq);
+    }
+  }
+  if (threadIdx.x == 0) {
+    SegPlan& P = L.plan;
+    P.start = 0;
+    P.len = n;
+    P.tile_base = 0;
+    P.group_base = 0;
+    P.ntiles = T;
+    P.ngroups = 1;
+    P.shift = shift;
+    P.bits = bits;
+    P.buf = src;
+    P.dst = BUF_TMP;
+    P.skip = 0;
+  }
+  // (the next tile's first two columns are loaded while this one is scattered)
+  uint64_t n0[IT], n1[IT];
+  auto load_next = [&](int t) {
+    const int64_t tbase = (int64_t)t * kTile;
+    const int cnt = tile_cnt(t);
+    load_strip<IT>(n0, desc->cols[0].base[src], desc->cols[0].width, desc->cols[0].stride[src],
+                   tbase, ebase, cnt);
+    if (ncols > 1)
+      load_strip<IT>(n1, desc->cols[1].base[src], desc->cols[1].width,
+                     desc->cols[1].stride[src], tbase, ebase, cnt);
+  };
+  if (w < T) load_next(w);
+  for (int t = w; t < T; t += G) {
+    const int cnt = tile_cnt(t);
+    const int64_t tbase = (int64_t)t * kTile;
+    uint64_t v0[IT], v1[IT], v2[IT];
+#pragma unroll
+    for (int k = 0; k < IT; k++) {
+      v0[k] = n0[k];
+      v1[k] = n1[k];
+    }
+    const int64_t my_off = b < nb ? (int64_t)bs + mid_ld(&hist[(size_t)t * kMaxBins + b]) : 0;
+    if (t + G < T) load_next(t + G);  // (after the offsets' load: its wait skips these)
+    __syncthreads();  // (the plan is published; the previous tile's LDS use is over)
+    TileInfo ti;
+    ti.base = tbase;
+    ti.cnt = cnt;
+    ti.s = 0;
+    ti.t = t;
+    scatter_process_tile<KT, U, 0, CZ, false>(desc, &L.plan, L.sc, ti, ncols, v0, v1, v2, my_off,
+                                               DigitLut{});
+  }
+}
+
+// ---------------------------------------------------------------------------
 // sampled 16-bit key histogram (balanced first level): chunk c
 // = keys [c*stride, c*stride + chunk). Each of kSampleWGs workgroups counts
 // its share of the chunks into LDS-private u16 bins (64K bins packed in
@@ -4261,6 +4543,48 @@ hipError_t launch_mid_sort(int key_size, const SortDesc& d, int64_t n, int src,
 #define CALL(KT, U, CZ)                                                                         \
   mid_sort_kernel<KT, U, CZ><<<G, kLocalThreads, 0, st>>>(d, n, src, part, hist, ctr, big,    \
                                                           taken, flag, seq, bar, wide);       \
+  return hipGetLastError()
+  SRS_KEY_DISPATCH(key_size, CALL)
+#undef CALL
+  return hipErrorInvalidValue;
+}
+
+int64_t mid_level_part_bytes() { return (int64_t)(kMaxBins + 2 * kMidLevelMaxTiles) * 8; }
+
+hipError_t launch_mid_level(int key_size, const SortDesc& d, int64_t n, int src,
+                            unsigned long long* part, uint32_t* hist, ListCounters* ctr, Seg* big,
+                            Seg* local, Seg* local2, Seg* copy, SortDesc* d_out, MidFlag* flag,
+                            unsigned long long seq, unsigned long long* bar, hipStream_t st) {
+  const int64_t T = (n + kTile - 1) / kTile;
+  if (n <= 0 || T > kMidLevelMaxTiles) return hipErrorInvalidValue;
+  // the grid: as many workgroups as stay resident together (the grid
+  // barriers), at most one per tile; cached per device and key dispatch
+  static std::atomic<int> cap_cache[64][6];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return hipErrorInvalidValue;
+  const int kb = key_size & 0xff;
+  const int slot = (key_size & SRS_KS_CANON) ? (kb == 4 ? 4 : 5) : kb == 1 ? 0 : kb == 2 ? 1 : kb == 4 ? 2 : 3;
+  int resident = cap_cache[dev][slot].load(std::memory_order_relaxed);
+  if (resident == 0) {
+    int cus = 0, per_cu = 0;
+    hipError_t oe = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+#define OCC(KT, U, CZ)                                                                            \
+  if (oe == hipSuccess)                                                                          \
+    oe = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, mid_level_kernel<KT, U, CZ>,      \
+                                                      kScatterThreads, 0)
+    SRS_KEY_DISPATCH(key_size, OCC)
+#undef OCC
+    if (oe != hipSuccess) return oe;
+    resident = std::max(1, cus * per_cu);
+    if (per_cu < 1) resident = -1;
+    cap_cache[dev][slot].store(resident, std::memory_order_relaxed);
+  }
+  if (resident < 0) return hipErrorCooperativeLaunchTooLarge;
+  const unsigned G = (unsigned)std::min<int64_t>(T, resident);
+#define CALL(KT, U, CZ)                                                                          \
+  mid_level_kernel<KT, U, CZ><<<G, kScatterThreads, 0, st>>>(d, n, src, part, hist, ctr, big,   \
+                                                             local, local2, copy, d_out, flag,  \
+                                                             seq, bar);                         \
   return hipGetLastError()
   SRS_KEY_DISPATCH(key_size, CALL)
 #undef CALL

@@ -14,6 +14,8 @@
 #   shardspan8   the same over keys confined to 1/8 of the key range (one of 8 ranks' span)
 #   profiles     tools/round_profiles.sh $PROFILE_TAG (C1 / C2 / C3 traces + PMC passes)
 #   lat          tools/latency.py over the small / mid sizes
+#   latab        tools/latency.py at 1M-4M keys without / with the mid-level launch
+#   phases       tools/latency_phases.py (kernel time per family), without / with the mid-level launch
 #   bench        the default bench.py line (what the driver runs)
 # After a crash, abort or time limit (rc >= 124, 134, 139) nothing else runs.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -22,6 +24,7 @@ shift
 mkdir -p "$OUT"
 : > "$OUT/steps.txt"
 export TMPDIR=/tmp
+LATN="1048577 1500000 2097152 3000000 3900000 4194304 6000000"
 PT="python -u -m pytest -x -q --timeout 240 --timeout-method thread -m gpu"
 step() {  # name timeout cmd...
   local name=$1 to=$2; shift 2
@@ -52,6 +55,10 @@ for s in "$@"; do
                  --cpu-sample 0 ;;
     profiles) step profiles 1500 bash tools/round_profiles.sh "${PROFILE_TAG:-r06}" ;;
     lat) step latency 300 python tools/latency.py ;;
+    latab) step latency_general 300 env SRS_MID_LEVEL_MAX=0 python tools/latency.py $LATN &&
+           step latency_midlevel 300 python tools/latency.py $LATN ;;
+    phases) step phases_general 300 env SRS_MID_LEVEL_MAX=0 python tools/latency_phases.py $LATN &&
+            step phases_midlevel 300 python tools/latency_phases.py $LATN ;;
     bench) step bench_default 900 python bench.py ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
