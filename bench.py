@@ -725,14 +725,48 @@ def alloc_variants(args, step_args, torch, srs_amd):
     def restore():
         for w, s_ in zip(work, src):
             w.copy_(s_)
+
+    def split(fn, prep=None):
+        # one more step with HIP-event markers around every launch: which
+        # kernels the unplaced memory slows down (ms per launch)
+        if prep:
+            prep()
+        torch.cuda.synchronize()
+        srs_amd.reset_kernel_stats()
+        srs_amd.set_kernel_timing(True)
+        try:
+            fn()
+            torch.cuda.synchronize()
+        finally:
+            srs_amd.set_kernel_timing(False)
+        out = {}
+        for name in ("count", "scan", "local", "scatter.L1", "scatter.L2"):
+            try:
+                l, ms, _ = srs_amd.kernel_stats(name)
+            except Exception:
+                continue
+            if l:
+                out[name] = round(ms / l, 4)
+        return out
+
+    # the placement probe's write rate of each buffer (ms per GB; DESIGN.md
+    # §4: a slow-class buffer probes slow) before anything is written to it
+    probe = {}
+    if hasattr(srs_amd, "debug_probe_write"):
+        for name, bufs in (("plain_alloc", outs), ("inplace", work)):
+            probe[name] = [round(srs_amd.debug_probe_write(t.data_ptr(), t.numel() * t.element_size())
+                                 / (t.numel() * t.element_size() / 1e9), 4) for t in bufs]
     plain, plain_all = timed(lambda: sort(src, tuple(outs)))
     inplace, inplace_all = timed(lambda: sort(work, None), prep=restore)
     ok = all(torch.equal(w, o) for w, o in zip(work, outs))
+    kern = {"plain_alloc": split(lambda: sort(src, tuple(outs))),
+            "inplace": split(lambda: sort(work, None), prep=restore)}
     del outs, work
     torch.cuda.empty_cache()
     return {"ms_per_step_plain_alloc": plain, "ms_per_step_inplace": inplace,
             "alloc_variants": {"steps": k, "plain_alloc_ms": plain_all, "inplace_ms": inplace_all,
                                "inplace_equals_out_of_place": ok,
+                               "kernel_ms_per_launch": kern, "probe_ms_per_gb": probe,
                                "note": "outputs from torch's allocator / sorted in place on a "
                                        "torch array restored from the input before each step; "
                                        "median of the steps (the headline's outputs come from "

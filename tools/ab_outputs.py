@@ -7,7 +7,10 @@ local times (the kernels that write the outputs), and the placement probe's
 ms per GB of each output column (srs_debug_probe_write), to see whether the
 probe ranks the buffers the way the sort does.
 
-usage: python tools/ab_outputs.py [--sets placed,plain,placed,plain] [--rounds 7]
+"inplace" arms sort a torch array in place (restored from the input before
+each step, untimed): the reference's in-place contract.
+
+usage: python tools/ab_outputs.py [--sets placed,plain,inplace,placed] [--rounds 7]
 """
 import argparse
 import json
@@ -39,26 +42,42 @@ def main():
     for i, kind in enumerate(a.sets.split(",")):
         if kind == "placed":
             outs = [srs_amd.empty_device(n, torch.int64, dev) for _ in range(2)]
+        elif kind == "inplace":  # (the caller's own arrays, restored before each step)
+            outs = [torch.empty(n, dtype=torch.int64, device=dev) for _ in range(2)]
         else:
             outs = [torch.empty(n, dtype=torch.int64, device=dev) for _ in range(2)]
         torch.cuda.synchronize()
         probe = [round(srs_amd.debug_probe_write(o.data_ptr(), o.numel() * 8) / (o.numel() * 8 / 1e9), 4)
                  for o in outs]
         arms.append({"name": f"{i}:{kind}", "outs": outs, "probe_ms_per_gb": probe,
-                     "step_ms": [], "scatter.L2": [], "local": [], "scatter.L1": []})
+                     "inplace": kind == "inplace", "step_ms": [], "scatter.L2": [], "local": [],
+                     "scatter.L1": [], "count": [], "scan": []})
+    def run(arm):
+        if arm["inplace"]:
+            srs_amd.sort_device(*arm["outs"], key_kind=srs_amd.KEY_U64)
+        else:
+            srs_amd.sort_device(keys, pays, key_kind=srs_amd.KEY_U64, out=tuple(arm["outs"]))
+
+    def restore(arm):
+        if arm["inplace"]:
+            arm["outs"][0].copy_(keys)
+            arm["outs"][1].copy_(pays)
+
     for arm in arms:  # warmup
-        srs_amd.sort_device(keys, pays, key_kind=srs_amd.KEY_U64, out=tuple(arm["outs"]))
+        restore(arm)
+        run(arm)
     torch.cuda.synchronize()
     srs_amd.set_kernel_timing(True)
     for _ in range(a.rounds):
         for arm in arms:
+            restore(arm)
             srs_amd.reset_kernel_stats()
             torch.cuda.synchronize()
             t0 = time.perf_counter()
-            srs_amd.sort_device(keys, pays, key_kind=srs_amd.KEY_U64, out=tuple(arm["outs"]))
+            run(arm)
             torch.cuda.synchronize()
             arm["step_ms"].append((time.perf_counter() - t0) * 1e3)
-            for k in ("scatter.L1", "scatter.L2", "local"):
+            for k in ("scatter.L1", "scatter.L2", "local", "count", "scan"):
                 l, ms, _ = srs_amd.kernel_stats(k)
                 if l:
                     arm[k].append(ms / l)
@@ -66,7 +85,7 @@ def main():
     print(json.dumps({"n": n, "rounds": a.rounds, "arms": [
         {"arm": arm["name"], "probe_ms_per_gb": arm["probe_ms_per_gb"],
          **{k: round(statistics.median(arm[k]), 4) for k in ("step_ms", "scatter.L1", "scatter.L2",
-                                                              "local") if arm[k]}}
+                                                              "local", "count", "scan") if arm[k]}}
         for arm in arms]}))
 
 
