@@ -368,6 +368,12 @@ int srs_debug_set_stamp_buffer(void* device_acc);
  * (mismatches, spin timeouts, look-back hops of digit 0). NULL disables. */
 int srs_debug_set_lookback(void* status, void* err);
 
+/* The super-group column scan: a level over one large segment
+ * scans sums of 64 scan groups once it has at least min_groups groups of 32
+ * tiles (default 256, i.e. 33.5 M keys; <= 0 restores it). Process-wide;
+ * tests lower it so that the path runs at small sizes. */
+int srs_debug_set_super_scan(int64_t min_groups);
+
 /* Segments the local-level fallback kernels took in the last sort on the
  * current device: counts[0] = handed to the stable kernel, counts[1] = handed
  * on to the LSD kernel. Synchronizes the device. Tests use it to prove that

@@ -30,6 +30,10 @@ void launch_count(int key_size, const SortDesc* d, const SegPlan* plan,
 int64_t scan_temp_elems(int64_t n);
 void launch_excl_scan(const uint64_t* x, uint64_t* y, int64_t n, uint64_t* temp,
                       uint64_t* total, hipStream_t st);
+// rows launch_offsets' super-group scan adds behind gsum's and gofs' group rows
+int64_t super_rows(int64_t ngroups);
+// the scan groups from which a one-segment level takes it (<= 0: the default, 256)
+void set_super_scan_min_groups(int64_t g);
 void launch_offsets(SegPlan* plan, int64_t nbig, const int32_t* group_seg, int64_t ngroups,
                     const uint16_t* hist, uint32_t* gsum, uint64_t* gofs, uint64_t* sbase,
                     uint64_t* offs, uint32_t* offs32, const unsigned long long* var_or,

@@ -1183,7 +1183,9 @@ __global__ __launch_bounds__(kMaxBins) void seg_scan_kernel(
     uint64_t* __restrict__ gofs, uint64_t* __restrict__ sbase,
     const unsigned long long* __restrict__ var_or, Seg* big_next, Seg* local, Seg* local2,
     Seg* copy, ListCounters* ctr, const int32_t* __restrict__ lut_rbits, int mode,
-    uint32_t* __restrict__ prun) {
+    uint32_t* __restrict__ prun, int64_t rows) {
+  // rows > 0: the one segment's scan over `rows` super-group rows (gsum /
+  // gofs then hold the super sums / offsets; launch_offsets).
   // mode 0: a plain level. 1: a stripe level (every stripe is scattered, its
   // bucket sizes go to prun; the next level's segments come from
   // stripe_segs_kernel). 2: a gathered level (every segment is scattered:
@@ -1197,8 +1199,24 @@ __global__ __launch_bounds__(kMaxBins) void seg_scan_kernel(
   if (b == 0) single = 0;
   uint64_t run = 0;
   if (b < nb) {
-    const int64_t g0 = P.group_base, g1 = P.group_base + P.ngroups;
+    const int64_t g0 = rows > 0 ? 0 : P.group_base;
+    const int64_t g1 = rows > 0 ? rows : P.group_base + P.ngroups;
     int64_t g = g0;
+    // One thread walks its bin's column serially, so a segment of many
+    // groups is bound by load latency (one whole segment of 1e9 / 4 keys:
+    // 2348 groups, 0.19-0.47 ms per launch at four loads per step): 32 group
+    // sums in flight per step
+    constexpr int U = 32;
+    for (; g + U <= g1; g += U) {
+      uint32_t a[U];
+#pragma unroll
+      for (int k = 0; k < U; k++) a[k] = gsum[(g + k) * kMaxBins + b];
+#pragma unroll
+      for (int k = 0; k < U; k++) {
+        gofs[(g + k) * kMaxBins + b] = run;
+        run += a[k];
+      }
+    }
     for (; g + 4 <= g1; g += 4) {
       const uint32_t a0 = gsum[(g + 0) * kMaxBins + b], a1 = gsum[(g + 1) * kMaxBins + b];
       const uint32_t a2 = gsum[(g + 2) * kMaxBins + b], a3 = gsum[(g + 3) * kMaxBins + b];
@@ -4334,6 +4352,65 @@ void launch_excl_scan(const uint64_t* x, uint64_t* y, int64_t n, uint64_t* temp,
   if (nb > 0) scan_apply_kernel<<<(unsigned)nb, kScanThreads, 0, st>>>(x, n, temp, y);
 }
 
+// SRS_SUPER_SCAN=0: the one-workgroup column scan for every segment (A/B)
+bool super_scan_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("SRS_SUPER_SCAN");
+    return !(e && *e == '0');
+  }();
+  return on;
+}
+
+// One large segment (a shard's partition chunk or round sort, any level of
+// a single big segment): its column scan is one workgroup, i.e. one CU
+// moving ngroups x 6 KB of rows (2348 groups of a 250 M-key chunk: 14 MB,
+// 0.17-0.47 ms). Above kSuperMinGroups groups the scan runs
+// over sums of kSuperGroups groups instead, and a grid-wide pass turns the
+// super offsets back into group offsets.
+constexpr int64_t kSuperGroups = 64;
+constexpr int64_t kSuperMinGroups = 256;
+int64_t g_super_min_groups = kSuperMinGroups;  // (srs_debug_set_super_scan)
+
+void set_super_scan_min_groups(int64_t g) { g_super_min_groups = g > 0 ? g : kSuperMinGroups; }
+
+int64_t super_rows(int64_t ngroups) { return (ngroups + kSuperGroups - 1) / kSuperGroups; }
+
+__global__ __launch_bounds__(kMaxBins) void super_sum_kernel(const SegPlan* __restrict__ plan,
+                                                             const uint32_t* __restrict__ gsum,
+                                                             int64_t ngroups,
+                                                             uint32_t* __restrict__ ssum) {
+  const uint32_t b = threadIdx.x;
+  if (b >= (1u << plan[0].bits)) return;
+  const int64_t g0 = (int64_t)blockIdx.x * kSuperGroups;
+  const int64_t g1 = min(g0 + kSuperGroups, ngroups);
+  uint32_t s0 = 0, s1 = 0, s2 = 0, s3 = 0;  // (<= 64 x 32 tiles x 4096 keys: fits 32 bits)
+  int64_t g = g0;
+  for (; g + 4 <= g1; g += 4) {
+    s0 += gsum[(g + 0) * kMaxBins + b];
+    s1 += gsum[(g + 1) * kMaxBins + b];
+    s2 += gsum[(g + 2) * kMaxBins + b];
+    s3 += gsum[(g + 3) * kMaxBins + b];
+  }
+  for (; g < g1; g++) s0 += gsum[g * kMaxBins + b];
+  ssum[(int64_t)blockIdx.x * kMaxBins + b] = s0 + s1 + s2 + s3;
+}
+
+__global__ __launch_bounds__(kMaxBins) void super_apply_kernel(const SegPlan* __restrict__ plan,
+                                                               const uint32_t* __restrict__ gsum,
+                                                               int64_t ngroups,
+                                                               const uint64_t* __restrict__ sofs,
+                                                               uint64_t* __restrict__ gofs) {
+  const uint32_t b = threadIdx.x;
+  if (plan[0].skip || b >= (1u << plan[0].bits)) return;
+  const int64_t g0 = (int64_t)blockIdx.x * kSuperGroups;
+  const int64_t g1 = min(g0 + kSuperGroups, ngroups);
+  uint64_t run = sofs[(int64_t)blockIdx.x * kMaxBins + b];
+  for (int64_t g = g0; g < g1; g++) {
+    gofs[g * kMaxBins + b] = run;
+    run += gsum[g * kMaxBins + b];
+  }
+}
+
 void launch_offsets(SegPlan* plan, int64_t nbig, const int32_t* group_seg, int64_t ngroups,
                     const uint16_t* hist, uint32_t* gsum, uint64_t* gofs, uint64_t* sbase,
                     uint64_t* offs, uint32_t* offs32, const unsigned long long* var_or,
@@ -4341,9 +4418,21 @@ void launch_offsets(SegPlan* plan, int64_t nbig, const int32_t* group_seg, int64
                     Seg* local, Seg* local2, Seg* copy, ListCounters* ctr,
                     const int32_t* lut_rbits, hipStream_t st, int mode, uint32_t* prun) {
   group_sum_kernel<<<(unsigned)ngroups, kMaxBins, 0, st>>>(plan, group_seg, hist, gsum);
-  seg_scan_kernel<<<(unsigned)nbig, kMaxBins, 0, st>>>(plan, gsum, gofs, sbase, var_or,
-                                                      big_next, local, local2, copy, ctr,
-                                                      lut_rbits, mode, prun);
+  if (nbig == 1 && mode != 1 && ngroups >= g_super_min_groups && super_scan_enabled()) {
+    // (the super rows live behind the group rows: the caller sizes gsum and
+    // gofs for ngroups + super_rows(ngroups) rows)
+    const int64_t ns = super_rows(ngroups);
+    uint32_t* ssum = gsum + ngroups * kMaxBins;
+    uint64_t* sofs = gofs + ngroups * kMaxBins;
+    super_sum_kernel<<<(unsigned)ns, kMaxBins, 0, st>>>(plan, gsum, ngroups, ssum);
+    seg_scan_kernel<<<1, kMaxBins, 0, st>>>(plan, ssum, sofs, sbase, var_or, big_next, local,
+                                            local2, copy, ctr, lut_rbits, mode, prun, ns);
+    super_apply_kernel<<<(unsigned)ns, kMaxBins, 0, st>>>(plan, gsum, ngroups, sofs, gofs);
+  } else {
+    seg_scan_kernel<<<(unsigned)nbig, kMaxBins, 0, st>>>(plan, gsum, gofs, sbase, var_or,
+                                                        big_next, local, local2, copy, ctr,
+                                                        lut_rbits, mode, prun, 0);
+  }
   tile_offs_kernel<<<(unsigned)ngroups, kMaxBins, 0, st>>>(
       plan, group_seg, hist, gofs, sbase, offs, offs32);
 }

@@ -1316,8 +1316,16 @@ int srs_shard_sort_multi(int32_t num_devices, const srs_shard_comm* comms, const
       if (rc[i] != SRS_OK) err[i] = srs_last_error();
     });
   for (auto& t : th) t.join();
+  // every failing rank's own message (a rank that only learnt of a peer's
+  // failure from a status collective says so; the peer's message says why)
+  int first = SRS_OK;
+  std::string msg;
   for (int i = 0; i < num_devices; i++)
-    if (rc[i] != SRS_OK) return set_error(rc[i], "rank " + std::to_string(i) + ": " + err[i]);
+    if (rc[i] != SRS_OK) {
+      if (first == SRS_OK) first = rc[i];
+      msg += (msg.empty() ? "" : "; ") + ("rank " + std::to_string(i) + ": " + err[i]);
+    }
+  if (first != SRS_OK) return set_error(first, msg);
   return SRS_OK;
 }
 

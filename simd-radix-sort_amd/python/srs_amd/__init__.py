@@ -80,6 +80,7 @@ def lib() -> ctypes.CDLL:
     L.srs_partition_device.argtypes = [i64, ctypes.c_int, ctypes.c_int, vp, i32, vp, vp,
                                        ctypes.c_int, vp, i32, vp, vp, vp, vp]
     L.srs_debug_last_fallbacks.argtypes = [ctypes.POINTER(i64)]
+    L.srs_debug_set_super_scan.argtypes = [i64]
     L.srs_debug_last_local_counts.argtypes = [ctypes.POINTER(i64)]
     L.srs_debug_last_local_classes.argtypes = [ctypes.POINTER(i64)]
     L.srs_set_host_devices.argtypes = [i32, vp]
@@ -453,6 +454,12 @@ def debug_alloc(nbytes: int, mode: int = 0) -> int:
 
 def debug_free(ptr: int) -> None:
     _check(lib().srs_debug_free(ctypes.c_void_p(ptr)))
+
+
+def debug_set_super_scan(min_groups: int) -> None:
+    """Scan groups from which a one-segment level takes the super-group
+    column scan (srs_debug_set_super_scan; 0 = the default, 256)."""
+    _check(lib().srs_debug_set_super_scan(int(min_groups)))
 
 
 def debug_probe_write(ptr: int, nbytes: int) -> float:
